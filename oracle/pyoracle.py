@@ -1,0 +1,198 @@
+"""ctypes binding of oracle/liboracle.so (the CPU restatement, oracle.c).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and
+bench.py's cpu_baseline leg, as the checker / CPU baseline. The product
+package (nav-slam_amd/) never imports this module.
+"""
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(HERE, "liboracle.so")
+
+_dp = C.POINTER(C.c_double)
+_ip = C.POINTER(C.c_int)
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", HERE], check=True)
+
+
+def _d(a):
+    return a.ctypes.data_as(_dp)
+
+
+def _i(a):
+    return a.ctypes.data_as(_ip)
+
+
+class Oracle:
+    def __init__(self):
+        if not os.path.exists(LIB):
+            build()
+        L = self.L = C.CDLL(LIB)
+        L.orc_convert_to_pointcloud.argtypes = [_ip, C.c_int, C.c_int, _dp]
+        L.orc_extract_feature.argtypes = [_dp, C.c_int, C.c_int, _ip, C.c_void_p]
+        L.orc_rotation_matrix_deg.argtypes = [C.c_double] * 3 + [_dp]
+        L.orc_transform_cloud.argtypes = [_dp, C.c_size_t, _dp, _dp, _dp]
+        L.orc_kd_build.argtypes = [_dp, _ip, C.c_size_t]
+        L.orc_kd_nn.argtypes = [_dp, C.c_size_t, _dp, C.POINTER(C.c_long), _dp]
+        L.orc_rows_match.argtypes = [_dp, _dp, C.c_int, C.c_int, _ip, _ip, _ip, _dp]
+        L.orc_knn_brute.argtypes = [_dp, C.c_size_t, _dp, C.c_size_t, C.c_int, _ip, _dp]
+        L.orc_slam_create.restype = C.c_void_p
+        L.orc_slam_create.argtypes = [C.c_int, C.c_int]
+        L.orc_slam_destroy.argtypes = [C.c_void_p]
+        L.orc_slam_init.argtypes = [C.c_void_p, _dp, _dp]
+        L.orc_slam_localization.argtypes = [C.c_void_p, _dp, _dp, _dp, _dp, _ip, _ip]
+        L.orc_slam_mapping.argtypes = [C.c_void_p, _dp, _dp]
+        L.orc_slam_error.restype = C.c_double
+        L.orc_slam_error.argtypes = [C.c_void_p]
+        L.orc_slam_frame_count.restype = C.c_int
+        L.orc_slam_frame_count.argtypes = [C.c_void_p]
+        L.orc_slam_tree.restype = C.c_size_t
+        L.orc_slam_tree.argtypes = [C.c_void_p, C.c_int, C.POINTER(_dp), C.POINTER(_ip)]
+        L.orc_slam_last_global.restype = _dp
+        L.orc_slam_last_global.argtypes = [C.c_void_p]
+        for f in ("orc_ekf_init", "orc_ekf_predict", "orc_ekf_modify"):
+            getattr(L, f).argtypes = [C.c_void_p, _dp] + ([_dp] if f == "orc_ekf_predict" else [])
+        L.orc_ekf_update_R.argtypes = [C.c_void_p, C.c_double]
+
+    # ---- single functions -------------------------------------------------
+    def convert(self, depth):
+        depth = np.ascontiguousarray(depth, np.int32)
+        R, Cc = depth.shape
+        out = np.zeros((R, Cc, 3))
+        self.L.orc_convert_to_pointcloud(_i(depth), R, Cc, _d(out))
+        return out
+
+    def extract_feature(self, pts, want_curv=False):
+        pts = np.ascontiguousarray(pts, np.float64)
+        R, Cc = pts.shape[:2]
+        mask = np.zeros((R, Cc), np.int32)
+        curv = np.zeros((R, Cc)) if want_curv else None
+        self.L.orc_extract_feature(_d(pts), R, Cc, _i(mask),
+                                   curv.ctypes.data if want_curv else None)
+        return (mask, curv) if want_curv else mask
+
+    def rotation(self, roll, pitch, yaw):
+        Rm = np.zeros(9)
+        self.L.orc_rotation_matrix_deg(roll, pitch, yaw, _d(Rm))
+        return Rm
+
+    def transform(self, pts, pos6):
+        pts = np.ascontiguousarray(pts, np.float64)
+        Rm = self.rotation(pos6[3], pos6[4], pos6[5])
+        t = np.ascontiguousarray(pos6[:3], np.float64)
+        out = np.zeros_like(pts)
+        self.L.orc_transform_cloud(_d(pts), pts.size // 3, _d(Rm), _d(t), _d(out))
+        return out
+
+    def kd_build(self, pts):
+        """Returns (permuted points, permutation of original indices)."""
+        p = np.array(pts, np.float64, order="C").reshape(-1, 3)
+        ix = np.arange(len(p), dtype=np.int32)
+        self.L.orc_kd_build(_d(p), _i(ix), len(p))
+        return p, ix
+
+    def kd_nn(self, tree, q):
+        tree = np.ascontiguousarray(tree, np.float64).reshape(-1, 3)
+        q = np.ascontiguousarray(q, np.float64)
+        pos = C.c_long()
+        d = np.zeros(1)
+        self.L.orc_kd_nn(_d(tree), len(tree), _d(q), C.byref(pos), _d(d))
+        return pos.value, d[0]
+
+    def rows_match(self, src, tgt):
+        src = np.ascontiguousarray(src, np.float64)
+        tgt = np.ascontiguousarray(tgt, np.float64)
+        R, Cc = src.shape[:2]
+        sm = np.zeros((R, Cc), np.int32)
+        tm = np.zeros((R, Cc), np.int32)
+        idx = np.zeros((R, Cc), np.int32)
+        dist = np.zeros((R, Cc))
+        self.L.orc_rows_match(_d(src), _d(tgt), R, Cc, _i(sm), _i(tm), _i(idx), _d(dist))
+        return sm, tm, idx, dist
+
+    def knn_brute(self, tgt, qs, k):
+        tgt = np.ascontiguousarray(tgt, np.float64).reshape(-1, 3)
+        qs = np.ascontiguousarray(qs, np.float64).reshape(-1, 3)
+        idx = np.zeros((len(qs), k), np.int32)
+        dist = np.zeros((len(qs), k))
+        self.L.orc_knn_brute(_d(tgt), len(tgt), _d(qs), len(qs), k, _i(idx), _d(dist))
+        return idx, dist
+
+
+class OracleSlam:
+    """src/slam.c:134-431 frame loop at runtime dims (oracle restatement)."""
+
+    def __init__(self, orc, R, Cc):
+        self.o, self.R, self.C = orc, R, Cc
+        self.h = orc.L.orc_slam_create(R, Cc)
+
+    def __del__(self):
+        try:
+            self.o.L.orc_slam_destroy(self.h)
+        except Exception:
+            pass
+
+    def init(self, pos6, lidar):
+        self.o.L.orc_slam_init(self.h, _d(np.ascontiguousarray(pos6, np.float64)),
+                               _d(np.ascontiguousarray(lidar, np.float64)))
+
+    def localization(self, lidar, pred6, last6):
+        out = np.zeros(6)
+        it = np.zeros(1, np.int32)
+        nc = np.zeros(1, np.int32)
+        self.o.L.orc_slam_localization(self.h, _d(np.ascontiguousarray(lidar, np.float64)),
+                                       _d(np.ascontiguousarray(pred6, np.float64)),
+                                       _d(np.ascontiguousarray(last6, np.float64)),
+                                       _d(out), _i(it), _i(nc))
+        return out, int(it[0]), int(nc[0])
+
+    def mapping(self, pos6, lidar):
+        self.o.L.orc_slam_mapping(self.h, _d(np.ascontiguousarray(pos6, np.float64)),
+                                  _d(np.ascontiguousarray(lidar, np.float64)))
+
+    @property
+    def error(self):
+        return self.o.L.orc_slam_error(self.h)
+
+    @property
+    def frame_count(self):
+        return self.o.L.orc_slam_frame_count(self.h)
+
+    def tree(self, r):
+        p = _dp()
+        c = _ip()
+        n = self.o.L.orc_slam_tree(self.h, r, C.byref(p), C.byref(c))
+        pts = np.ctypeslib.as_array(p, (max(n, 1) * 3,))[: 3 * n].reshape(-1, 3).copy()
+        cols = np.ctypeslib.as_array(c, (max(n, 1),))[:n].copy()
+        return pts, cols
+
+    def last_global(self):
+        g = self.o.L.orc_slam_last_global(self.h)
+        return np.ctypeslib.as_array(g, (self.R * self.C * 3,)).reshape(self.R, self.C, 3).copy()
+
+
+class OracleEkf:
+    def __init__(self, orc, pos6):
+        self.o = orc
+        self.buf = np.zeros(6 + 3 * 36)
+        orc.L.orc_ekf_init(self.buf.ctypes.data, _d(np.ascontiguousarray(pos6, np.float64)))
+
+    def predict(self, last6, cur6):
+        self.o.L.orc_ekf_predict(self.buf.ctypes.data, _d(np.asarray(last6, np.float64)),
+                                 _d(np.asarray(cur6, np.float64)))
+
+    def modify(self, meas6):
+        self.o.L.orc_ekf_modify(self.buf.ctypes.data, _d(np.asarray(meas6, np.float64)))
+
+    def update_R(self, err):
+        self.o.L.orc_ekf_update_R(self.buf.ctypes.data, float(err))
+
+    @property
+    def pos(self):
+        return self.buf[:6].copy()
