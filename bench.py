@@ -1,0 +1,297 @@
+#!/usr/bin/env python3
+"""Scan-pair matches/sec on MI355X (BASELINE.json metric), one process per GPU.
+
+Default workload (K3, BASELINE.json configs[2] — the config the metric is
+quoted on, "1M-pt clouds"): one scan pair per GPU, 1,048,576 points per cloud
+arranged as a 512x2048 grid, x,y,z ~ U[0,1000) mm. One step = the whole
+front end on that pair, inputs already resident in HBM:
+    curvature/features of source and target (R1)
+  + index build over the target (radix-binned uniform grid)
+  + exact k=8 nearest neighbours of every source point.
+value = matches (query points matched) over all ranks / max-over-ranks time.
+
+`--workload k2` runs the per-row slam.c mode instead (128x2048 L9-shaped
+pair, 1-NN, exact reference KD semantics) and `--workload k4` a batch of
+256 K2 pairs sharded over the ranks with an RCCL all-gather of the match
+sets (the north star's batched case).
+
+Launch: python bench.py [--gpus N --steps K --warmup W]; for N > 1 under
+torch.distributed.run (one rank per GPU, RCCL).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "nav-slam_amd"))
+
+import numpy as np  # noqa: E402
+
+METRIC = ("scan-pair matches/sec (feature-extract + kNN), 1M-pt clouds, 1/2/4/8 MI355X; "
+          "% HBM roofline")
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (8.0 TB/s spec)
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--workload", choices=["k3", "k2", "k4"], default="k3")
+    p.add_argument("--k", type=int, default=8)
+    p.add_argument("--rows", type=int, default=None)
+    p.add_argument("--cols", type=int, default=None)
+    p.add_argument("--pairs", type=int, default=256, help="k4: total pairs")
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cpu-reps", type=int, default=3)
+    p.add_argument("--traffic-csv", default=None,
+                   help="rocprofv3 --pmc counter_collection.csv to derive HBM bytes")
+    p.add_argument("--json-out", default=None)
+    return p.parse_args()
+
+
+def dist_env():
+    ws = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    return ws, rank, local
+
+
+def cpu_baseline_k3(src, tgt, k, reps):
+    """The reference's own CPU path on the same pair (rank 0 only):
+    oracle/_ref/libref8x8.so = utils/kdtree.c compiled as-is (buildKDTree over
+    the 1M target, nearestNeighborSearch for every source point; the
+    reference implements k=1 only) + the oracle's bit-exact restatement of
+    extract_feature on both 512x2048 clouds (the reference's is fixed to
+    8x8). Single-threaded like the reference; median of `reps` runs."""
+    import ctypes as C
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    from pyoracle import Oracle
+    orc = Oracle()
+    ref_path = os.path.join(ROOT, "oracle", "_ref", "libref8x8.so")
+    kind = "reference" if os.path.exists(ref_path) else "port"
+    N = src.shape[0] * src.shape[1]
+    times = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        orc.extract_feature(src)
+        orc.extract_feature(tgt)
+        if kind == "reference":
+            lib = C.CDLL(ref_path)
+            lib.buildKDTree.restype = C.c_void_p
+            lib.buildKDTree.argtypes = [C.c_void_p, C.c_size_t, C.c_int]
+            lib.freeKDTree.argtypes = [C.c_void_p]
+            lib.nearestNeighborSearch.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p,
+                                                  C.c_void_p, C.c_int]
+            arr = np.ascontiguousarray(tgt.reshape(-1, 3)).copy()
+            root = lib.buildKDTree(arr.ctypes.data, N, 0)
+            fn = C.cast(lib.nearestNeighborSearch, C.c_void_p).value
+            orc.ref_nn_batch(fn, root, src.reshape(-1, 3))
+            lib.freeKDTree(root)
+        else:
+            t, _ = orc.kd_build(tgt.reshape(-1, 3))
+            orc.kd_nn_batch(t, src.reshape(-1, 3))
+        times.append(time.perf_counter() - t0)
+    t = float(np.median(times))
+    return {"value": N / t, "unit": "matches/s", "cores": 1, "kind": kind,
+            "seconds_per_pair": t,
+            "sample": (f"the full K3 pair ({N} queries vs {N} targets), median of {reps}: "
+                       "extract_feature on both clouds + buildKDTree + nearestNeighborSearch "
+                       "per source point, k=1 (the reference has no k-NN; k=8 would cost "
+                       "more)")}
+
+
+def main():
+    a = parse()
+    ws, rank, local = dist_env()
+    import torch
+    import torch.distributed as dist
+    if ws > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local if ws > 1 else 0)
+    torch.cuda.set_device(dev)
+    from navslam import synth
+    from navslam.gpu import NavGpu
+
+    stream = torch.cuda.current_stream(dev)
+    g = NavGpu(dev.index, stream.cuda_stream)
+
+    if a.workload == "k3":
+        R = a.rows or 512
+        Cc = a.cols or 2048
+        src_h, tgt_h = synth.uniform_pair(R, Cc, seed_src=1 + 2 * rank, seed_tgt=2 + 2 * rank)
+        N = R * Cc
+        src = torch.from_numpy(src_h).to(dev)
+        tgt = torch.from_numpy(tgt_h).to(dev)
+        sm = torch.empty((R, Cc), dtype=torch.int32, device=dev)
+        tm = torch.empty((R, Cc), dtype=torch.int32, device=dev)
+        idx = torch.empty((N, a.k), dtype=torch.int32, device=dev)
+        dst = torch.empty((N, a.k), dtype=torch.float64, device=dev)
+
+        def step():
+            g.pair_knn_dev(src, tgt, R, Cc, a.k, sm, tm, idx, dst)
+        matches_per_step = N
+        dom = "knn_query"
+        dom_bytes = (24 + 24 + 12 * a.k) * N        # 24Q + 24T + 12kQ
+        path_bytes = 2 * 28 * N + dom_bytes          # + curvature 28 B/pt, both clouds
+        path_kernels = ["curvature", "knn_query"]
+        workload = (f"K3: {N}-point scan pair ({R}x{Cc} grid, U[0,1000)^3 mm), curvature "
+                    f"on both clouds + grid index build + exact k={a.k} NN of every source "
+                    "point, global mode")
+        data = "synthetic: x,y,z ~ U[0,1000) mm, numpy PCG64 seeds (1+2r, 2+2r) on rank r"
+        cfg_extra = {"points_per_cloud": N, "k": a.k, "pairs_per_gpu": 1, "mode": "global"}
+    else:
+        R = a.rows or 128
+        Cc = a.cols or 2048
+        N = R * Cc
+        if a.workload == "k2":
+            pairs = 1
+        else:
+            pairs = max(1, a.pairs // ws)
+        srcs, tgts = [], []
+        for p in range(pairs):
+            s_h, t_h = synth.l9_pair(R, Cc, seed=1000 * rank + p + 5)
+            srcs.append(torch.from_numpy(s_h).to(dev))
+            tgts.append(torch.from_numpy(t_h).to(dev))
+            if a.workload == "k4" and p >= 7:   # reuse 8 distinct pairs, cycled
+                break
+        nd = len(srcs)
+        sm = torch.empty((pairs, R, Cc), dtype=torch.int32, device=dev)
+        tm = torch.empty((pairs, R, Cc), dtype=torch.int32, device=dev)
+        idx = torch.empty((pairs, R, Cc), dtype=torch.int32, device=dev)
+        dst = torch.empty((pairs, R, Cc), dtype=torch.float64, device=dev)
+        gather_buf = None
+        if a.workload == "k4" and ws > 1:
+            gather_buf = torch.empty((ws * pairs, R, Cc), dtype=torch.int32, device=dev)
+
+        def step():
+            for p in range(pairs):
+                g.rows_match_dev(srcs[p % nd], tgts[p % nd], R, Cc, sm[p], tm[p], idx[p], dst[p])
+            if gather_buf is not None:
+                dist.all_gather_into_tensor(gather_buf, idx)
+        # matches = feature queries actually searched (constant per pair)
+        step()
+        torch.cuda.synchronize()
+        matches_per_step = int((sm[: min(pairs, nd)] == 1).sum().item()) * (pairs // min(pairs, nd)) \
+            + int((sm[: pairs % min(pairs, nd)] == 1).sum().item())
+        dom = "rows_match"
+        dom_bytes = None
+        path_bytes = None
+        path_kernels = ["rows_match"]
+        workload = (f"{'K2' if a.workload == 'k2' else 'K4'}: {pairs} L9-shaped {R}x{Cc} "
+                    "scan pair(s) per GPU, per-row mode (slam.c semantics): curvature of both "
+                    "clouds + exact reference KD per target row + 1-NN of every source feature"
+                    + (", RCCL all-gather of the match sets" if gather_buf is not None else ""))
+        data = "synthetic L9-shaped range images (navslam.synth.l9_pair), fixed seeds"
+        cfg_extra = {"points_per_cloud": N, "k": 1, "pairs_per_gpu": pairs, "mode": "rows"}
+
+    # warmup (grows the workspace, JITs nothing)
+    for _ in range(a.warmup):
+        step()
+    torch.cuda.synchronize()
+    if ws > 1:
+        dist.barrier()
+    g.timing(True)
+    for name in set(path_kernels + [dom]):
+        g.timing_read(name, reset=True)
+    torch.cuda.synchronize()
+    if ws > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        step()
+    torch.cuda.synchronize()
+    if ws > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
+    g.timing(False)
+    elapsed = t1 - t0
+    if ws > 1:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+    kt = {}
+    for name in set(path_kernels + [dom]):
+        ms, n = g.timing_read(name, reset=True)
+        kt[name] = (ms, n)
+
+    out = None
+    if rank == 0:
+        ms_per_step = 1000.0 * elapsed / a.steps
+        value = ws * matches_per_step * a.steps / elapsed
+        dom_ms, dom_n = kt.get(dom, (0.0, 0))
+        dom_avg_us = 1000.0 * dom_ms / max(dom_n, 1)
+        roof = None
+        if dom_bytes is not None and dom_n > 0:
+            ach = dom_bytes / (dom_avg_us * 1e-6) / 1e9
+            traffic = None
+            if a.traffic_csv:
+                traffic = traffic_from_csv(a.traffic_csv, "k_knn")
+            roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
+                    "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic,
+                    "kernel": "k_knn<%d>" % a.k, "avg_us": round(dom_avg_us, 2),
+                    "bytes_per_launch": dom_bytes,
+                    "bytes_model": "24 B/query read + 24 B/target read + 12*k B/query out"}
+        elif dom_n > 0:
+            roof = {"bound": "hbm", "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": None, "traffic": None, "kernel": dom,
+                    "avg_us": round(dom_avg_us, 2),
+                    "note": "latency/LDS-bound per-row kernel; bytes model in DESIGN.md"}
+        path = None
+        if path_bytes is not None:
+            tot_us = 0.0
+            for kname in path_kernels:
+                ms, n = kt.get(kname, (0.0, 0))
+                tot_us += 1000.0 * ms / max(a.steps, 1)
+            if tot_us > 0:
+                pa = path_bytes / (tot_us * 1e-6) / 1e9
+                path = {"kernels_us_per_step": round(tot_us, 2), "bytes_per_step": path_bytes,
+                        "achieved": round(pa, 1), "frac": round(pa / HBM_PEAK_GBS, 4)}
+        cpu = None
+        if ws == 1 and not a.no_cpu_baseline and a.workload == "k3":
+            cpu = cpu_baseline_k3(src_h, tgt_h, a.k, a.cpu_reps)
+        out = {"metric": METRIC, "value": round(value, 1), "unit": "matches/s",
+               "n_gpus": ws, "steps": a.steps, "warmup": a.warmup,
+               "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
+               "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": data,
+               "config": dict({"workload": workload, "parallelism": f"replicas x{ws}"},
+                              **cfg_extra),
+               "roofline": roof, "curvature_plus_query": path,
+               "kernel_us": {k: round(1000.0 * v[0] / max(v[1], 1), 2) for k, v in kt.items()},
+               "cpu_baseline": cpu}
+        line = json.dumps(out)
+        print(line, flush=True)
+        if a.json_out:
+            with open(a.json_out, "w") as f:
+                f.write(line + "\n")
+    g.close()
+    if ws > 1:
+        dist.destroy_process_group()
+    return out
+
+
+def traffic_from_csv(path, kernel_sub):
+    """Per-launch HBM bytes of `kernel_sub` from a rocprofv3 counter CSV
+    (FETCH_SIZE doubled per MI355X_MICROARCH.md §HBM, + WRITE_SIZE; KB)."""
+    import csv
+    fetch, write, n = 0.0, 0.0, set()
+    with open(path) as f:
+        for r in csv.DictReader(f):
+            if kernel_sub not in r.get("Kernel_Name", ""):
+                continue
+            n.add(r.get("Dispatch_Id"))
+            v = float(r.get("Counter_Value", 0))
+            if r.get("Counter_Name") == "FETCH_SIZE":
+                fetch += v
+            elif r.get("Counter_Name") == "WRITE_SIZE":
+                write += v
+    if not n:
+        return None
+    return round((2 * fetch + write) * 1024 / len(n))
+
+
+if __name__ == "__main__":
+    main()

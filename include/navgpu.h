@@ -1,0 +1,179 @@
+/*
+ * navgpu.h — C ABI of the MI355X scan-matching core (libnavgpu.so).
+ *
+ * Plain pointers and sizes, no C++/torch types. Two families of entry points:
+ *
+ *  *_dev : inputs and outputs are DEVICE pointers (hipMalloc'd or any HIP
+ *          allocation, e.g. a torch tensor's data_ptr()), enqueued on the
+ *          context's stream, asynchronous, no host synchronisation and no
+ *          allocation once the workspace has grown to the shape (so a warm
+ *          call can be captured into a hipGraph).
+ *  *_host: the same computation on HOST pointers: copy in, run, copy out,
+ *          synchronise. These back the drop-in C shim (slam.h / kdtree.h /
+ *          pointcloud.h, see include/slam.h).
+ *
+ * Clouds are `double[R*C*3]`, row-major, x,y,z interleaved: the reference
+ * `Point ToF_position[MAX_ROWS][MAX_COLS]` (utils/pointcloud.h:32-44) with
+ * runtime R, C. Every function returns NAVGPU_OK or a negative status; the
+ * message of the last failure is navgpu_last_error(). There is NO CPU
+ * fallback: without a usable gfx950 device every compute call fails.
+ *
+ * Reference functions each entry point replaces (file:line in
+ * wuHakureReimu/NAV-SLAM):
+ *   navgpu_curvature_*     extract_feature            src/slam.c:11-61
+ *   navgpu_project_*       convertToPointCloud        utils/pointcloud.c:8-48
+ *   navgpu_kd_build_rows_* flattenPoints+buildKDTree  src/slam.c:64-81,
+ *                                                     utils/kdtree.c:8-82
+ *   navgpu_kd_query_rows_* nearestNeighborSearch loop src/slam.c:236-244,
+ *                                                     utils/kdtree.c:110-152
+ *   navgpu_rows_match_*    the per-row scan-pair composition:
+ *                          extract_feature x2 + per-row build + 1-NN
+ *   navgpu_knn_*           global-mode k-NN (the reference has k = 1 only;
+ *                          ordering = (distance, index))
+ */
+#ifndef NAVGPU_H
+#define NAVGPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define NAVGPU_OK 0
+#define NAVGPU_EINVAL (-1)  /* bad argument / shape                      */
+#define NAVGPU_EHIP (-2)    /* HIP runtime error (no device, fault, ...) */
+#define NAVGPU_ENOMEM (-3)  /* device allocation failed                   */
+#define NAVGPU_ERANGE (-4)  /* shape beyond what a kernel supports        */
+
+typedef struct navgpu_ctx navgpu_ctx;
+
+/* Context = device + stream + grow-only workspace. stream may be NULL (a
+ * private non-blocking stream is created) or a hipStream_t to enqueue on. */
+int navgpu_create(int device, void *stream, navgpu_ctx **out);
+void navgpu_destroy(navgpu_ctx *ctx);
+int navgpu_set_stream(navgpu_ctx *ctx, void *stream);
+void *navgpu_stream(navgpu_ctx *ctx);
+int navgpu_sync(navgpu_ctx *ctx);
+const char *navgpu_last_error(void);
+const char *navgpu_version(void);
+/* Largest row width the in-LDS row kernels accept (depends on the device's
+ * LDS size); larger rows return NAVGPU_ERANGE. */
+int navgpu_rows_max_cols(void);
+
+/* ---- R1: curvature / edge features (src/slam.c:11-61) -------------------
+ * mask[r*C+c] = 1 iff the reference marks (r,c) a feature, else 0 (the
+ * reference writes only 1s into a caller-zeroed array). curv (nullable)
+ * receives the curvature value (0 where none is computed). */
+int navgpu_curvature_dev(navgpu_ctx *ctx, const double *pts, int R, int C,
+                         int32_t *mask, double *curv);
+int navgpu_curvature_host(navgpu_ctx *ctx, const double *pts, int R, int C,
+                          int32_t *mask, double *curv);
+
+/* ---- R2: depth grid -> points (utils/pointcloud.c:8-48) ----------------- */
+int navgpu_project_dev(navgpu_ctx *ctx, const int32_t *depth, int R, int C,
+                       double *pts);
+int navgpu_project_host(navgpu_ctx *ctx, const int32_t *depth, int R, int C,
+                        double *pts);
+
+/* ---- R3: rigid transform (src/slam.c:95-131,145-160,193-210) ------------
+ * out = t + Rm*p (Rm row-major 3x3, the reference's left-to-right sums);
+ * when out_last != NULL also out_last = out - tr (mapCoordinatesToLastFrame).
+ * Rm is passed from the host so no device transcendental is involved. */
+int navgpu_transform_dev(navgpu_ctx *ctx, const double *pts, size_t n,
+                         const double Rm[9], const double t[3],
+                         const double tr[3], double *out, double *out_last);
+
+/* ---- R4+R5: per-row feature trees ---------------------------------------
+ * For each row r: the feature points of `coords` row r (feature = mask of
+ * `feat_src`, computed here with R1; coords and feat_src may be the same
+ * cloud) compacted in column order (flattenPoints) and arranged by the
+ * reference's exact buildKDTree permutation (Lomuto nth_element, median
+ * n/2, axis depth%3). Outputs, per row r at offset r*C:
+ *   tree_pts[3*(r*C+i)] : i-th point of the permuted array (== implicit
+ *                         tree: node of [lo,hi) at lo+(hi-lo)/2)
+ *   tree_col[r*C+i]     : its column; tree_n[r]: count.
+ * mask_out (nullable) receives the feature mask. */
+int navgpu_kd_build_rows_dev(navgpu_ctx *ctx, const double *feat_src,
+                             const double *coords, int R, int C,
+                             double *tree_pts, int32_t *tree_col,
+                             int32_t *tree_n, int32_t *mask_out);
+
+/* ---- R6: per-row 1-NN over the trees of navgpu_kd_build_rows ------------
+ * Queries = feature points of `feat_src` (mask via R1), coordinates from
+ * `queries`; query (r,c) searches tree r exactly like
+ * nearestNeighborSearch (first-visited point wins ties). Per grid cell:
+ *   nn_pos[r*C+c]  = tree position (index into row r of tree_pts), -1 if
+ *                    (r,c) is not a feature or tree r is empty;
+ *   nn_dist[r*C+c] = reference distance, +INFINITY when nn_pos == -1.
+ * mask_out (nullable) receives the query feature mask. */
+int navgpu_kd_query_rows_dev(navgpu_ctx *ctx, const double *tree_pts,
+                             const int32_t *tree_n, const double *feat_src,
+                             const double *queries, int R, int C,
+                             int32_t *nn_pos, double *nn_dist,
+                             int32_t *mask_out);
+
+/* ---- The K2 scan-pair step, per-row mode (fused, one kernel) ------------
+ * masks of src and tgt (R1), per-row target trees (R4+R5), every src
+ * feature queried against its row's tree (R6). nn_idx = linear target index
+ * r*C+c of the nearest point (-1: not a feature / empty row tree),
+ * nn_dist as above. src_mask / tgt_mask nullable. */
+int navgpu_rows_match_dev(navgpu_ctx *ctx, const double *src,
+                          const double *tgt, int R, int C, int32_t *src_mask,
+                          int32_t *tgt_mask, int32_t *nn_idx, double *nn_dist);
+int navgpu_rows_match_host(navgpu_ctx *ctx, const double *src,
+                           const double *tgt, int R, int C, int32_t *src_mask,
+                           int32_t *tgt_mask, int32_t *nn_idx,
+                           double *nn_dist);
+
+/* ---- Global-mode k-NN (K3) ----------------------------------------------
+ * For each of nq queries the k (1..16) target points with the smallest
+ * reference distance sqrt((dx*dx+dy*dy)+dz*dz), dx = target - query,
+ * ordered by (distance, index) ascending. idx[q*k+s] / dist[q*k+s]; slots
+ * left unfilled get -1 / +INFINITY. As in the reference 1-NN (a candidate
+ * is taken only if dist < best, best starting at +INFINITY), a target whose
+ * distance is +INFINITY or NaN is never a neighbour. Index: a radix-binned uniform grid over the
+ * target cloud, rebuilt every call. */
+int navgpu_knn_dev(navgpu_ctx *ctx, const double *tgt, size_t nt,
+                   const double *queries, size_t nq, int k, int32_t *idx,
+                   double *dist);
+int navgpu_knn_host(navgpu_ctx *ctx, const double *tgt, size_t nt,
+                    const double *queries, size_t nq, int k, int32_t *idx,
+                    double *dist);
+
+/* The K3 scan-pair step: curvature masks of both R x C clouds + global k-NN
+ * of every src point against tgt. Masks nullable. */
+int navgpu_pair_knn_dev(navgpu_ctx *ctx, const double *src, const double *tgt,
+                        int R, int C, int k, int32_t *src_mask,
+                        int32_t *tgt_mask, int32_t *idx, double *dist);
+
+/* ---- R5 for one arbitrary point array (kdtree.h buildKDTree) ------------
+ * pts: n points (AoS), permuted in place into the reference's buildKDTree
+ * order for a root at depth `depth0` (axis = (depth0 + level) % 3).
+ * n up to INT32_MAX; rows that fit the LDS build in LDS, larger arrays use a
+ * global-memory scratch of the same algorithm. */
+int navgpu_kd_build_dev(navgpu_ctx *ctx, double *pts, size_t n, int depth0);
+int navgpu_kd_build_host(navgpu_ctx *ctx, double *pts, size_t n, int depth0);
+
+/* ---- device memory helpers (for C callers without HIP headers) --------- */
+int navgpu_malloc(navgpu_ctx *ctx, size_t bytes, void **dptr);
+void navgpu_free(navgpu_ctx *ctx, void *dptr);
+/* stream-ordered copies on the context's stream (host memory pageable) */
+int navgpu_upload(navgpu_ctx *ctx, void *dst_dev, const void *src_host,
+                  size_t bytes);
+int navgpu_download(navgpu_ctx *ctx, void *dst_host, const void *src_dev,
+                    size_t bytes);
+
+/* Kernel-level timing hook for bench.py: HIP events recorded around the
+ * dominant kernel of the last *_dev call on the context's stream. Returns
+ * the summed milliseconds of the named kernel since the last reset
+ * (name: "knn_query", "rows_match", "curvature"), or -1. */
+void navgpu_timing_enable(navgpu_ctx *ctx, int on);
+double navgpu_timing_read(navgpu_ctx *ctx, const char *name, int reset);
+int navgpu_timing_count(navgpu_ctx *ctx, const char *name);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,1594 @@
+// navgpu.hip — MI355X (gfx950) kernels and C ABI of the NAV-SLAM scan-matching
+// front end (include/navgpu.h). Built with `-ffp-contract=off`, no fast-math:
+// every floating-point expression keeps the reference's association order so
+// masks, tree permutations, neighbours and distances are bit-identical to the
+// reference C path (wuHakureReimu/NAV-SLAM src/slam.c, utils/kdtree.c,
+// utils/pointcloud.c).
+//
+// Kernels (DESIGN.md has the HBM layout and the roofline of each):
+//   k_curvature      R1  row tiles + 2-point halo staged in LDS
+//   k_project        R2  depth grid -> xyz with host-computed tan tables
+//   k_transform      R3  t + R*p (and - tr), elementwise
+//   k_rows_match     R1+R4+R5+R6 fused per row: target-row features, exact
+//                    reference KD permutation built in LDS, source-row
+//                    feature queries against it, one workgroup per row
+//   k_rows_build / k_rows_query  the same split in two (slam.c keeps the
+//                    target trees across frames)
+//   k_bbox, k_grid_params, k_cell_count, k_scan_*, k_scatter, k_knn<K>
+//                    global mode: radix-binned uniform grid over the target
+//                    cloud + exact k-NN, (distance, index) ordering
+#include <hip/hip_runtime.h>
+
+#include <math.h>
+#include <stdarg.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <map>
+#include <string>
+#include <utility>
+#include <vector>
+
+#include "navgpu.h"
+
+#pragma clang fp contract(off)
+
+#define NAVGPU_VERSION "navgpu 0.1 (gfx950)"
+
+namespace {
+
+constexpr int kWave = 64;
+constexpr int kRowsBlock = 512;     // 8 waves per row workgroup
+constexpr int kStackDepth = 14;     // implicit-tree height bound, n < 8192
+constexpr int kMaxRowCols = 8191;   // 13-bit stack-entry fields
+constexpr int kCurvTile = 256;
+
+// ------------------------------------------------------------------ errors
+char g_err[1024] = "";
+
+void set_err(const char *fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof(g_err), fmt, ap);
+  va_end(ap);
+}
+
+#define HIP_TRY(expr)                                                          \
+  do {                                                                         \
+    hipError_t e_ = (expr);                                                    \
+    if (e_ != hipSuccess) {                                                    \
+      set_err("%s:%d %s: %s", __FILE__, __LINE__, #expr,                      \
+              hipGetErrorString(e_));                                          \
+      return NAVGPU_EHIP;                                                      \
+    }                                                                          \
+  } while (0)
+
+#define CHECK_LAUNCH(name)                                                     \
+  do {                                                                         \
+    hipError_t e_ = hipGetLastError();                                         \
+    if (e_ != hipSuccess) {                                                    \
+      set_err("launch %s: %s", name, hipGetErrorString(e_));                  \
+      return NAVGPU_EHIP;                                                      \
+    }                                                                          \
+  } while (0)
+
+#define ARG_CHECK(cond)                                                        \
+  do {                                                                         \
+    if (!(cond)) {                                                             \
+      set_err("invalid argument: %s", #cond);                                 \
+      return NAVGPU_EINVAL;                                                    \
+    }                                                                          \
+  } while (0)
+
+// ============================================================ device helpers
+
+// utils/kdtree.c:14-17 (euclideanDistance; gcc folds pow(v,2) to v*v) and
+// src/slam.c:28-33,47-50: sqrt((dx*dx + dy*dy) + dz*dz), no contraction.
+__device__ __forceinline__ double ref_dist(double ax, double ay, double az,
+                                           double bx, double by, double bz) {
+  const double dx = ax - bx, dy = ay - by, dz = az - bz;
+  return __builtin_sqrt(dx * dx + dy * dy + dz * dz);
+}
+
+// src/slam.c:15-58 for one point with its four same-row neighbours
+// (k = -2, -1, +1, +2 in that order). The four distances are computed once
+// and reused for the variance: sqrt is deterministic, so this is the
+// reference's second loop bit for bit.
+__device__ __forceinline__ double curvature5(const double *c, const double *m2,
+                                             const double *m1, const double *p1,
+                                             const double *p2) {
+  const double d0 = ref_dist(c[0], c[1], c[2], m2[0], m2[1], m2[2]);
+  const double d1 = ref_dist(c[0], c[1], c[2], m1[0], m1[1], m1[2]);
+  const double d2 = ref_dist(c[0], c[1], c[2], p1[0], p1[1], p1[2]);
+  const double d3 = ref_dist(c[0], c[1], c[2], p2[0], p2[1], p2[2]);
+  double sum = 0.0;
+  sum += d0;
+  sum += d1;
+  sum += d2;
+  sum += d3;
+  const int count = 4;
+  const double avg = sum / count;
+  double curv = 0.0;
+  if (avg > 0) {
+    double var = 0.0;
+    var += (d0 - avg) * (d0 - avg);
+    var += (d1 - avg) * (d1 - avg);
+    var += (d2 - avg) * (d2 - avg);
+    var += (d3 - avg) * (d3 - avg);
+    curv = var / count / (avg * avg + 1e-6f);
+  }
+  return curv;
+}
+
+// curvature of column j of a row held AoS in LDS (raw[3*j..]); 0 outside the
+// reference's window 2 <= j < C-2 (src/slam.c:16).
+__device__ __forceinline__ double row_curv_lds(const double *raw, int C, int j) {
+  if (j < 2 || j >= C - 2) return 0.0;
+  return curvature5(raw + 3 * j, raw + 3 * (j - 2), raw + 3 * (j - 1),
+                    raw + 3 * (j + 1), raw + 3 * (j + 2));
+}
+
+// Coalesced copy of n doubles global -> LDS by the whole block.
+__device__ __forceinline__ void block_copy(double *dst, const double *src,
+                                           int n) {
+  for (int i = threadIdx.x; i < n; i += blockDim.x) dst[i] = src[i];
+}
+
+__device__ __forceinline__ int lanes_below(unsigned long long bal) {
+  return __builtin_amdgcn_mbcnt_hi((unsigned)(bal >> 32),
+                                   __builtin_amdgcn_mbcnt_lo((unsigned)bal, 0u));
+}
+
+__device__ __forceinline__ void wave_sync_mem() {
+  // Cross-lane hand-off through memory inside one wavefront (LDS, or global
+  // scratch of the large-n build): workgroup-scope release/acquire makes the
+  // other lanes' stores visible; wave_barrier stops code motion across it.
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+
+// Block-wide exclusive scan of one int per thread. scratch: >= nwaves+1 ints.
+__device__ int block_excl_scan(int v, int *scratch, int *total) {
+  const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
+  const int nw = blockDim.x / kWave;
+  int incl = v;
+#pragma unroll
+  for (int o = 1; o < kWave; o <<= 1) {
+    int t = __shfl_up(incl, o, kWave);
+    if (lane >= o) incl += t;
+  }
+  if (lane == kWave - 1) scratch[wid] = incl;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int acc = 0;
+    for (int w = 0; w < nw; ++w) {
+      int t = scratch[w];
+      scratch[w] = acc;
+      acc += t;
+    }
+    scratch[nw] = acc;
+  }
+  __syncthreads();
+  const int res = scratch[wid] + incl - v;
+  *total = scratch[nw];
+  __syncthreads();
+  return res;
+}
+
+// Stable compaction of [0, C): flag(j) -> write(j, rank). Each thread owns a
+// contiguous chunk so ranks follow column order (flattenPoints order,
+// src/slam.c:64-72). Returns the count.
+template <class Flag, class Write>
+__device__ int block_compact(int C, int *scratch, Flag flag, Write write) {
+  const int per = (C + blockDim.x - 1) / blockDim.x;
+  const int j0 = threadIdx.x * per;
+  const int j1 = min(C, j0 + per);
+  int cnt = 0;
+  for (int j = j0; j < j1; ++j) cnt += flag(j) ? 1 : 0;
+  int total;
+  int off = block_excl_scan(cnt, scratch, &total);
+  for (int j = j0; j < j1; ++j)
+    if (flag(j)) write(j, off++);
+  __syncthreads();
+  return total;
+}
+
+// ------------------------------------------------------------------------
+// Exact reference KD build (utils/kdtree.c:20-82) in LDS.
+//
+// The build permutes the row's feature array in place; that permuted array
+// IS the tree (node of [lo,hi) at lo+(hi-lo)/2). P[pos] = feature id at tree
+// position pos; key coordinates in FC[axis*NS + id].
+//
+// nth_element is a Lomuto quickselect (pivot = last, `cmp <= 0` goes left).
+// One wave runs one nth_element; a partition pass walks the window in 64-event
+// chunks: small events are stable-compacted to the front (ballot + mbcnt);
+// the large ones follow the "tape" rule that reproduces Lomuto's swaps
+// exactly: tape[p] = large ? elem(p) : tape[#smalls before p], resolved within
+// a chunk by pointer jumping over lanes (DESIGN.md §KD build). The final
+// layout is smalls | pivot | tape[S+1..m) with tape[S] moved to `last`.
+// ------------------------------------------------------------------------
+template <class IdxT>
+__device__ void wave_nth_element(const double *key, IdxT *P, IdxT *T,
+                                 int first, int last, int nth, int lane) {
+  while (first < last) {
+    const int pe = (int)P[last];
+    const double pk = key[pe];
+    const int m = last - first;
+    int S = 0;
+    for (int cs = 0; cs < m; cs += kWave) {
+      const int p = cs + lane;
+      const bool act = p < m;
+      const int e = act ? (int)P[first + p] : 0;
+      const bool small = act && ((key[e] - pk) <= 0.0);  // kdtree.c:31-43
+      const unsigned long long bal = __ballot(small);
+      const int sp = S + lanes_below(bal);
+      int val = e;
+      bool res = true;
+      int ptr = 0;
+      if (small) {
+        if (sp < cs) {
+          val = (int)T[first + sp];
+        } else if (sp != p) {
+          res = false;
+          ptr = sp - cs;
+        }
+      }
+      while (__ballot(!res)) {
+        const int src = res ? lane : ptr;
+        const int sval = __shfl(val, src, kWave);
+        const int sres = __shfl((int)res, src, kWave);
+        const int sptr = __shfl(ptr, src, kWave);
+        if (!res) {
+          if (sres) {
+            val = sval;
+            res = true;
+          } else {
+            ptr = sptr;
+          }
+        }
+      }
+      wave_sync_mem();
+      if (act) T[first + p] = (IdxT)val;
+      if (small) P[first + sp] = (IdxT)e;
+      S += __popcll(bal);
+      wave_sync_mem();
+    }
+    for (int q = S + lane; q < m; q += kWave) {
+      const int v = (int)T[first + q];
+      P[q == S ? last : first + q] = (IdxT)v;
+    }
+    wave_sync_mem();
+    if (lane == 0) P[first + S] = (IdxT)pe;
+    wave_sync_mem();
+    const int i = first + S;
+    if (i == nth) break;
+    if (i < nth)
+      first = i + 1;
+    else
+      last = i - 1;
+  }
+}
+
+// buildKDTree over n points, level by level: every subarray of one depth is
+// independent; waves take subarrays round-robin. Range of node k at level d
+// comes from walking its bits down from the root. Root axis = depth0 % 3
+// (kdtree.c:70, getAxis(depth)).
+template <class IdxT>
+__device__ void block_build_kdtree(const double *FC, size_t NS, int n,
+                                   IdxT *P, IdxT *T, int depth0) {
+  const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
+  const int nw = blockDim.x / kWave;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) P[i] = (IdxT)i;
+  __syncthreads();
+  for (int depth = 0; (n >> depth) >= 2; ++depth) {
+    const double *key = FC + ((depth0 + depth) % 3) * NS;
+    const int nodes = 1 << depth;
+    for (int k = wid; k < nodes; k += nw) {
+      int lo = 0, hi = n;
+      for (int b = depth - 1; b >= 0; --b) {
+        const int mid = lo + (hi - lo) / 2;
+        if ((k >> b) & 1)
+          lo = mid + 1;
+        else
+          hi = mid;
+      }
+      const int len = hi - lo;
+      if (len >= 2) wave_nth_element<IdxT>(key, P, T, lo, hi - 1, lo + len / 2, lane);
+    }
+    __syncthreads();
+  }
+}
+
+// Stack entry of the far subtree still to visit: [flo, fhi) at depth d; the
+// parent node is flo-1 when the far side is the right child, fhi otherwise.
+__device__ __forceinline__ uint32_t stk_enc(int flo, int fhi, int right, int d) {
+  return (uint32_t)flo | ((uint32_t)fhi << 13) | ((uint32_t)right << 26) |
+         ((uint32_t)d << 27);
+}
+
+// utils/kdtree.c:110-152 over the implicit tree TX/TY/TZ[0..n): the
+// recursion's visit order (node, near subtree, then far subtree iff
+// |q[axis]-node[axis]| < best at that moment) with an explicit LIFO stack.
+__device__ __forceinline__ void kd_query(const double *TX, const double *TY,
+                                         const double *TZ, int n, double qx,
+                                         double qy, double qz, uint32_t *stk,
+                                         int stride, int *best_pos,
+                                         double *best_dist) {
+  double best = INFINITY;
+  int bpos = -1;
+  int lo = 0, hi = n, depth = 0, sp = 0;
+  while (true) {
+    while (lo < hi) {
+      const int mid = lo + ((hi - lo) >> 1);
+      const double nx = TX[mid], ny = TY[mid], nz = TZ[mid];
+      const double d = ref_dist(nx, ny, nz, qx, qy, qz);
+      if (d < best) {
+        best = d;
+        bpos = mid;
+      }
+      const int axis = depth % 3;
+      const double qa = axis == 0 ? qx : (axis == 1 ? qy : qz);
+      const double na = axis == 0 ? nx : (axis == 1 ? ny : nz);
+      const bool left = qa < na;
+      const int flo = left ? mid + 1 : lo;
+      const int fhi = left ? hi : mid;
+      if (flo < fhi) stk[(sp++) * stride] = stk_enc(flo, fhi, left ? 1 : 0, depth + 1);
+      if (left)
+        hi = mid;
+      else
+        lo = mid + 1;
+      ++depth;
+    }
+    bool resume = false;
+    while (sp > 0) {
+      const uint32_t e = stk[(--sp) * stride];
+      const int flo = e & 0x1fff, fhi = (e >> 13) & 0x1fff;
+      const int right = (e >> 26) & 1, d1 = (int)(e >> 27);
+      const int parent = right ? flo - 1 : fhi;
+      const int axis = (d1 - 1) % 3;
+      const double qa = axis == 0 ? qx : (axis == 1 ? qy : qz);
+      const double na =
+          axis == 0 ? TX[parent] : (axis == 1 ? TY[parent] : TZ[parent]);
+      if (fabs(qa - na) < best) {  // kdtree.c:147-151
+        lo = flo;
+        hi = fhi;
+        depth = d1;
+        resume = true;
+        break;
+      }
+    }
+    if (!resume) break;
+  }
+  *best_pos = bpos;
+  *best_dist = best;
+}
+
+// LDS carve-up of the row kernels (byte offsets, 16-B aligned).
+struct RowsLds {
+  int raw, fc, fcol, p, t, stk, scan, total;
+};
+
+__host__ __device__ inline int align16(int x) { return (x + 15) & ~15; }
+
+__host__ __device__ inline RowsLds rows_lds(int C, int nthreads, bool stack) {
+  RowsLds L;
+  int o = 0;
+  L.raw = o;  o += align16(24 * C);
+  L.fc = o;   o += align16(24 * C);
+  L.fcol = o; o += align16(2 * C);
+  L.p = o;    o += align16(2 * C);
+  L.t = o;    o += align16(2 * C);
+  L.stk = o;  o += stack ? align16(4 * nthreads * kStackDepth) : 0;
+  L.scan = o; o += align16(4 * 40);
+  L.total = o;
+  return L;
+}
+
+extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+
+// Target row r of `coords` (features from `feat_src`): mask -> LDS + global,
+// compact features into FC/FCOL, build the exact KD permutation P.
+// On return the block is synchronised; returns n.
+__device__ int row_stage_and_build(const double *feat_src, const double *coords,
+                                   int r, int C, const RowsLds &L,
+                                   int32_t *mask_out) {
+  double *raw = (double *)(smem + L.raw);
+  double *FC = (double *)(smem + L.fc);
+  uint16_t *FCOL = (uint16_t *)(smem + L.fcol);
+  uint16_t *P = (uint16_t *)(smem + L.p);
+  uint16_t *MK = (uint16_t *)(smem + L.t);
+  int *scan = (int *)(smem + L.scan);
+  const size_t rowoff = (size_t)r * C;
+  block_copy(raw, feat_src + 3 * rowoff, 3 * C);
+  __syncthreads();
+  for (int j = threadIdx.x; j < C; j += blockDim.x) {
+    const int f = row_curv_lds(raw, C, j) > 0.1 ? 1 : 0;  // src/slam.c:58
+    MK[j] = (uint16_t)f;
+    if (mask_out) mask_out[rowoff + j] = f;
+  }
+  __syncthreads();
+  const bool same = coords == feat_src;
+  const int NS = C;
+  const int n = block_compact(
+      C, scan, [&](int j) { return MK[j] != 0; },
+      [&](int j, int pos) {
+        const double *s = same ? raw + 3 * j : coords + 3 * (rowoff + j);
+        FC[pos] = s[0];
+        FC[NS + pos] = s[1];
+        FC[2 * NS + pos] = s[2];
+        FCOL[pos] = (uint16_t)j;
+      });
+  block_build_kdtree<uint16_t>(FC, NS, n, P, (uint16_t *)(smem + L.t), 0);
+  return n;
+}
+
+// -------------------------------------------------------------- R1 kernel
+__global__ __launch_bounds__(kCurvTile) void k_curvature(
+    const double *__restrict__ pts, int R, int C, int32_t *__restrict__ mask,
+    double *__restrict__ curv) {
+  __shared__ double tile[3 * (kCurvTile + 4)];
+  const int r = blockIdx.y;
+  const int c0 = blockIdx.x * kCurvTile;
+  const int lo = max(0, c0 - 2), hi = min(C, c0 + kCurvTile + 2);
+  const size_t rowoff = (size_t)r * C;
+  const double *src = pts + 3 * (rowoff + lo);
+  const int nd = 3 * (hi - lo);
+  for (int i = threadIdx.x; i < nd; i += kCurvTile) tile[i] = src[i];
+  __syncthreads();
+  const int j = c0 + threadIdx.x;
+  if (j >= C) return;
+  const double *t = tile + 3 * (j - lo);
+  double cv = 0.0;
+  if (j >= 2 && j < C - 2) cv = curvature5(t, t - 6, t - 3, t + 3, t + 6);
+  mask[rowoff + j] = cv > 0.1 ? 1 : 0;
+  if (curv) curv[rowoff + j] = cv;
+}
+
+// -------------------------------------------------------------- R2 kernel
+// utils/pointcloud.c:17-46; tan tables are computed on the host with libm.
+__global__ void k_project(const int32_t *__restrict__ depth, int R, int C,
+                          const double *__restrict__ tan_col,
+                          const double *__restrict__ tan_row,
+                          double *__restrict__ pts) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (size_t)R * C) return;
+  const int row = (int)(i / C), col = (int)(i % C);
+  const double d = depth[i];
+  double x = 0.0, y = 0.0, z = 0.0;
+  if (!(d <= 0)) {
+    x = d;
+    y = -(d)*tan_col[col];
+    z = -(d)*tan_row[row];
+  }
+  pts[3 * i] = x;
+  pts[3 * i + 1] = y;
+  pts[3 * i + 2] = z;
+}
+
+// -------------------------------------------------------------- R3 kernel
+struct Rigid {
+  double R[9], t[3], tr[3];
+};
+
+__global__ void k_transform(const double *__restrict__ pts, size_t n, Rigid g,
+                            double *__restrict__ out,
+                            double *__restrict__ out_last) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const double lx = pts[3 * i], ly = pts[3 * i + 1], lz = pts[3 * i + 2];
+  const double rx = g.R[0] * lx + g.R[1] * ly + g.R[2] * lz;
+  const double ry = g.R[3] * lx + g.R[4] * ly + g.R[5] * lz;
+  const double rz = g.R[6] * lx + g.R[7] * ly + g.R[8] * lz;
+  const double ox = g.t[0] + rx, oy = g.t[1] + ry, oz = g.t[2] + rz;
+  out[3 * i] = ox;
+  out[3 * i + 1] = oy;
+  out[3 * i + 2] = oz;
+  if (out_last) {  // src/slam.c:126-128
+    out_last[3 * i] = ox - g.tr[0];
+    out_last[3 * i + 1] = oy - g.tr[1];
+    out_last[3 * i + 2] = oz - g.tr[2];
+  }
+}
+
+// ------------------------------------------------- fused per-row K2 kernel
+__global__ __launch_bounds__(kRowsBlock) void k_rows_match(
+    const double *__restrict__ src, const double *__restrict__ tgt, int R,
+    int C, int32_t *__restrict__ src_mask, int32_t *__restrict__ tgt_mask,
+    int32_t *__restrict__ nn_idx, double *__restrict__ nn_dist) {
+  const RowsLds L = rows_lds(C, kRowsBlock, true);
+  const int r = blockIdx.x;
+  const size_t rowoff = (size_t)r * C;
+  const int n = row_stage_and_build(tgt, tgt, r, C, L, tgt_mask);
+  double *raw = (double *)(smem + L.raw);
+  double *FC = (double *)(smem + L.fc);
+  uint16_t *FCOL = (uint16_t *)(smem + L.fcol);
+  uint16_t *P = (uint16_t *)(smem + L.p);
+  uint16_t *T = (uint16_t *)(smem + L.t);
+  uint32_t *stk = (uint32_t *)(smem + L.stk);
+  int *scan = (int *)(smem + L.scan);
+  // materialise the tree in position order: raw <- SoA tree, T <- columns
+  double *TX = raw, *TY = raw + C, *TZ = raw + 2 * C;
+  for (int pos = threadIdx.x; pos < n; pos += blockDim.x) {
+    const int e = P[pos];
+    TX[pos] = FC[e];
+    TY[pos] = FC[C + e];
+    TZ[pos] = FC[2 * C + e];
+    T[pos] = FCOL[e];
+  }
+  __syncthreads();
+  // source row (AoS) -> FC region; its mask -> P region; query list -> FCOL
+  double *sraw = FC;
+  uint16_t *SM = P;
+  block_copy(sraw, src + 3 * rowoff, 3 * C);
+  __syncthreads();
+  for (int j = threadIdx.x; j < C; j += blockDim.x) {
+    const int f = row_curv_lds(sraw, C, j) > 0.1 ? 1 : 0;
+    SM[j] = (uint16_t)f;
+    if (src_mask) src_mask[rowoff + j] = f;
+    if (!f) {
+      nn_idx[rowoff + j] = -1;
+      nn_dist[rowoff + j] = INFINITY;
+    }
+  }
+  __syncthreads();
+  uint16_t *QL = FCOL;
+  const int nq = block_compact(
+      C, scan, [&](int j) { return SM[j] != 0; },
+      [&](int j, int pos) { QL[pos] = (uint16_t)j; });
+  for (int i = threadIdx.x; i < nq; i += blockDim.x) {
+    const int c = QL[i];
+    int bpos;
+    double bd;
+    kd_query(TX, TY, TZ, n, sraw[3 * c], sraw[3 * c + 1], sraw[3 * c + 2],
+             stk + threadIdx.x, blockDim.x, &bpos, &bd);
+    nn_idx[rowoff + c] = bpos >= 0 ? (int)(rowoff + T[bpos]) : -1;
+    nn_dist[rowoff + c] = bd;
+  }
+}
+
+// ------------------------------------------- split per-row build / query
+__global__ __launch_bounds__(kRowsBlock) void k_rows_build(
+    const double *__restrict__ feat_src, const double *__restrict__ coords,
+    int R, int C, double *__restrict__ tree_pts, int32_t *__restrict__ tree_col,
+    int32_t *__restrict__ tree_n, int32_t *__restrict__ mask_out) {
+  const RowsLds L = rows_lds(C, kRowsBlock, false);
+  const int r = blockIdx.x;
+  const size_t rowoff = (size_t)r * C;
+  const int n = row_stage_and_build(feat_src, coords, r, C, L, mask_out);
+  const double *FC = (const double *)(smem + L.fc);
+  const uint16_t *FCOL = (const uint16_t *)(smem + L.fcol);
+  const uint16_t *P = (const uint16_t *)(smem + L.p);
+  for (int pos = threadIdx.x; pos < n; pos += blockDim.x) {
+    const int e = P[pos];
+    double *o = tree_pts + 3 * (rowoff + pos);
+    o[0] = FC[e];
+    o[1] = FC[C + e];
+    o[2] = FC[2 * C + e];
+    tree_col[rowoff + pos] = FCOL[e];
+  }
+  if (threadIdx.x == 0) tree_n[r] = n;
+}
+
+__global__ __launch_bounds__(kRowsBlock) void k_rows_query(
+    const double *__restrict__ tree_pts, const int32_t *__restrict__ tree_n,
+    const double *__restrict__ feat_src, const double *__restrict__ queries,
+    int R, int C, int32_t *__restrict__ nn_pos, double *__restrict__ nn_dist,
+    int32_t *__restrict__ mask_out) {
+  const RowsLds L = rows_lds(C, kRowsBlock, true);
+  const int r = blockIdx.x;
+  const size_t rowoff = (size_t)r * C;
+  double *raw = (double *)(smem + L.raw);
+  double *TX = (double *)(smem + L.fc), *TY = TX + C, *TZ = TX + 2 * C;
+  uint16_t *QM = (uint16_t *)(smem + L.p);
+  uint32_t *stk = (uint32_t *)(smem + L.stk);
+  const int n = tree_n[r];
+  for (int pos = threadIdx.x; pos < n; pos += blockDim.x) {
+    const double *t = tree_pts + 3 * (rowoff + pos);
+    TX[pos] = t[0];
+    TY[pos] = t[1];
+    TZ[pos] = t[2];
+  }
+  block_copy(raw, feat_src + 3 * rowoff, 3 * C);
+  __syncthreads();
+  for (int j = threadIdx.x; j < C; j += blockDim.x) {
+    const int f = row_curv_lds(raw, C, j) > 0.1 ? 1 : 0;
+    QM[j] = (uint16_t)f;
+    if (mask_out) mask_out[rowoff + j] = f;
+  }
+  __syncthreads();
+  for (int j = threadIdx.x; j < C; j += blockDim.x) {
+    int bpos = -1;
+    double bd = INFINITY;
+    if (QM[j]) {
+      const double *q = queries + 3 * (rowoff + j);
+      kd_query(TX, TY, TZ, n, q[0], q[1], q[2], stk + threadIdx.x, blockDim.x,
+               &bpos, &bd);
+    }
+    nn_pos[rowoff + j] = bpos;
+    nn_dist[rowoff + j] = bd;
+  }
+}
+
+// ---------------------------------------- R5 for one arbitrary array
+// kdtree.h buildKDTree: n points, in place, root axis depth0 % 3.
+__global__ __launch_bounds__(1024) void k_kd_build_lds(double *__restrict__ pts,
+                                                       int n, int depth0) {
+  double *FC = (double *)smem;
+  uint16_t *P = (uint16_t *)(smem + align16(24 * n));
+  uint16_t *T = P + ((align16(2 * n)) / 2);
+  for (int i = threadIdx.x; i < 3 * n; i += blockDim.x) {
+    const int e = i / 3, a = i % 3;
+    FC[a * n + e] = pts[i];
+  }
+  __syncthreads();
+  block_build_kdtree<uint16_t>(FC, n, n, P, T, depth0);
+  for (int i = threadIdx.x; i < 3 * n; i += blockDim.x) {
+    const int pos = i / 3, a = i % 3;
+    pts[i] = FC[a * n + P[pos]];
+  }
+}
+
+__global__ __launch_bounds__(1024) void k_kd_build_global(
+    double *__restrict__ pts, int n, int depth0, double *__restrict__ FC,
+    uint32_t *__restrict__ P, uint32_t *__restrict__ T) {
+  for (size_t i = threadIdx.x; i < 3 * (size_t)n; i += blockDim.x) {
+    const size_t e = i / 3, a = i % 3;
+    FC[a * n + e] = pts[i];
+  }
+  __syncthreads();
+  block_build_kdtree<uint32_t>(FC, (size_t)n, n, P, T, depth0);
+  for (size_t i = threadIdx.x; i < 3 * (size_t)n; i += blockDim.x) {
+    const size_t pos = i / 3, a = i % 3;
+    pts[i] = FC[a * (size_t)n + P[pos]];
+  }
+}
+
+inline int kd_build_lds_bytes(int n) {
+  return align16(24 * n) + 2 * align16(2 * n);
+}
+
+// ============================================================ global mode
+struct GridParams {
+  double o[3];
+  double h, inv_h, delta;
+  int g[3];
+  int ncells;
+};
+
+struct __align__(16) Rec {  // sorted target record, 32 B
+  double x, y, z;
+  int idx, pad;
+};
+
+constexpr int kOcc = 3;  // target points per cell
+
+__device__ __forceinline__ unsigned long long ord_enc(double v) {
+  unsigned long long u = (unsigned long long)__double_as_longlong(v);
+  return (u >> 63) ? ~u : (u | 0x8000000000000000ull);
+}
+__device__ __forceinline__ double ord_dec(unsigned long long u) {
+  u = (u >> 63) ? (u & 0x7fffffffffffffffull) : ~u;
+  return __longlong_as_double((long long)u);
+}
+
+// bbox[0..2] = ordered-min, bbox[3..5] = ordered-max (memset 0xff / 0x00)
+__global__ __launch_bounds__(256) void k_bbox(const double *__restrict__ p,
+                                              size_t n,
+                                              unsigned long long *bbox) {
+  double mn[3] = {INFINITY, INFINITY, INFINITY};
+  double mx[3] = {-INFINITY, -INFINITY, -INFINITY};
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (size_t)gridDim.x * blockDim.x) {
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+      const double v = p[3 * i + a];
+      if (v == v && fabs(v) < INFINITY) {
+        mn[a] = fmin(mn[a], v);
+        mx[a] = fmax(mx[a], v);
+      }
+    }
+  }
+#pragma unroll
+  for (int a = 0; a < 3; ++a) {
+    for (int o = kWave / 2; o > 0; o >>= 1) {
+      mn[a] = fmin(mn[a], __shfl_xor(mn[a], o, kWave));
+      mx[a] = fmax(mx[a], __shfl_xor(mx[a], o, kWave));
+    }
+  }
+  if ((threadIdx.x & (kWave - 1)) == 0) {
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+      if (mn[a] <= mx[a]) {
+        atomicMin(&bbox[a], ord_enc(mn[a]));
+        atomicMax(&bbox[3 + a], ord_enc(mx[a]));
+      }
+    }
+  }
+}
+
+__global__ void k_grid_params(const unsigned long long *bbox, size_t n,
+                              int cap, GridParams *gp) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  GridParams G;
+  double lo[3], ext[3];
+  bool any = true;
+  for (int a = 0; a < 3; ++a) {
+    const double l = ord_dec(bbox[a]), h = ord_dec(bbox[3 + a]);
+    if (!(l <= h)) any = false;
+    lo[a] = l;
+    ext[a] = h - l;
+  }
+  if (!any || n == 0) {
+    for (int a = 0; a < 3; ++a) {
+      G.o[a] = 0.0;
+      G.g[a] = 1;
+    }
+    G.h = 1.0;
+    G.inv_h = 1.0;
+    G.delta = 1.0;
+    G.ncells = 1;
+    *gp = G;
+    return;
+  }
+  const double emax = fmax(ext[0], fmax(ext[1], ext[2]));
+  const double floor_e = fmax(emax * 1e-6, 1e-9);
+  double vol = 1.0;
+  for (int a = 0; a < 3; ++a) vol *= fmax(ext[a], floor_e);
+  double h = cbrt(vol * kOcc / (double)n);
+  if (!(h > 0)) h = 1.0;
+  int g[3];
+  for (int it = 0; it < 64; ++it) {
+    long long tot = 1;
+    for (int a = 0; a < 3; ++a) {
+      double ga = ceil(ext[a] / h);
+      if (ga < 1) ga = 1;
+      if (ga > 1024) ga = 1024;
+      g[a] = (int)ga;
+      tot *= g[a];
+    }
+    if (tot <= cap) break;
+    h *= 1.26;
+  }
+  for (int a = 0; a < 3; ++a) G.o[a] = lo[a];
+  G.h = h;
+  G.inv_h = 1.0 / h;
+  G.delta = 1e-7 * (emax + h);
+  G.g[0] = g[0];
+  G.g[1] = g[1];
+  G.g[2] = g[2];
+  G.ncells = g[0] * g[1] * g[2];
+  *gp = G;
+}
+
+__device__ __forceinline__ int cell_axis(double v, const GridParams &G, int a) {
+  const double t = (v - G.o[a]) * G.inv_h;
+  if (!(t >= 0.0)) return 0;
+  if (t >= (double)G.g[a]) return G.g[a] - 1;
+  return (int)t;
+}
+
+__global__ __launch_bounds__(256) void k_cell_count(
+    const double *__restrict__ p, size_t n, const GridParams *__restrict__ gp,
+    int *__restrict__ cnt, int *__restrict__ cellid, int *__restrict__ slot) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const GridParams G = *gp;
+  const int cx = cell_axis(p[3 * i], G, 0), cy = cell_axis(p[3 * i + 1], G, 1),
+            cz = cell_axis(p[3 * i + 2], G, 2);
+  const int c = (cz * G.g[1] + cy) * G.g[0] + cx;
+  cellid[i] = c;
+  slot[i] = atomicAdd(&cnt[c], 1);
+}
+
+constexpr int kScanBlock = 1024, kScanPer = 4,
+              kScanTile = kScanBlock * kScanPer;
+
+__global__ __launch_bounds__(kScanBlock) void k_scan_sums(
+    const int *__restrict__ in, int n, int *__restrict__ bsum) {
+  __shared__ int scratch[40];
+  const int base = blockIdx.x * kScanTile + threadIdx.x * kScanPer;
+  int s = 0;
+#pragma unroll
+  for (int k = 0; k < kScanPer; ++k)
+    if (base + k < n) s += in[base + k];
+  int total;
+  block_excl_scan(s, scratch, &total);
+  if (threadIdx.x == 0) bsum[blockIdx.x] = total;
+}
+
+__global__ __launch_bounds__(kScanBlock) void k_scan_top(int *bsum, int nb) {
+  __shared__ int scratch[40];
+  // nb <= kScanBlock * kScanPer
+  int v[kScanPer];
+  int s = 0;
+#pragma unroll
+  for (int k = 0; k < kScanPer; ++k) {
+    const int i = threadIdx.x * kScanPer + k;
+    v[k] = i < nb ? bsum[i] : 0;
+    s += v[k];
+  }
+  int total;
+  int off = block_excl_scan(s, scratch, &total);
+#pragma unroll
+  for (int k = 0; k < kScanPer; ++k) {
+    const int i = threadIdx.x * kScanPer + k;
+    if (i < nb) bsum[i] = off;
+    off += v[k];
+  }
+}
+
+__global__ __launch_bounds__(kScanBlock) void k_scan_apply(
+    const int *__restrict__ in, int n, const int *__restrict__ bsum,
+    int *__restrict__ out) {
+  __shared__ int scratch[40];
+  const int base = blockIdx.x * kScanTile + threadIdx.x * kScanPer;
+  int v[kScanPer];
+  int s = 0;
+#pragma unroll
+  for (int k = 0; k < kScanPer; ++k) {
+    v[k] = base + k < n ? in[base + k] : 0;
+    s += v[k];
+  }
+  int total;
+  int off = block_excl_scan(s, scratch, &total) + bsum[blockIdx.x];
+#pragma unroll
+  for (int k = 0; k < kScanPer; ++k) {
+    if (base + k < n) out[base + k] = off;
+    off += v[k];
+  }
+}
+
+__global__ __launch_bounds__(256) void k_scatter(
+    const double *__restrict__ p, size_t n, const int *__restrict__ cellid,
+    const int *__restrict__ slot, const int *__restrict__ start,
+    Rec *__restrict__ rec) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  Rec r;
+  r.x = p[3 * i];
+  r.y = p[3 * i + 1];
+  r.z = p[3 * i + 2];
+  r.idx = (int)i;
+  r.pad = 0;
+  rec[start[cellid[i]] + slot[i]] = r;
+}
+
+// (d, i) < (kd, ki): distance first, then index. Never true for d = inf/NaN.
+__device__ __forceinline__ bool knn_less(double d, int i, double kd, int ki) {
+  return d < kd || (d == kd && i < ki);
+}
+
+template <int K>
+__global__ __launch_bounds__(256) void k_knn(
+    const GridParams *__restrict__ gp, const int *__restrict__ start,
+    const int *__restrict__ cnt, const Rec *__restrict__ rec,
+    const double *__restrict__ qs, size_t nq, int32_t *__restrict__ oidx,
+    double *__restrict__ odist) {
+  const size_t q = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= nq) return;
+  const GridParams G = *gp;
+  const double qx = qs[3 * q], qy = qs[3 * q + 1], qz = qs[3 * q + 2];
+  double kd[K];
+  int ki[K];
+#pragma unroll
+  for (int s = 0; s < K; ++s) {
+    kd[s] = INFINITY;
+    ki[s] = -1;
+  }
+  double thr = INFINITY;  // dsq admission bound for the current k-th
+  const int c[3] = {cell_axis(qx, G, 0), cell_axis(qy, G, 1),
+                    cell_axis(qz, G, 2)};
+  const double qv[3] = {qx, qy, qz};
+  const int gmax = max(G.g[0], max(G.g[1], G.g[2]));
+  for (int r = 0; r <= gmax; ++r) {
+    for (int dz = -r; dz <= r; ++dz) {
+      const int z = c[2] + dz;
+      if (z < 0 || z >= G.g[2]) continue;
+      for (int dy = -r; dy <= r; ++dy) {
+        const int y = c[1] + dy;
+        if (y < 0 || y >= G.g[1]) continue;
+        const bool face = (dz == -r || dz == r || dy == -r || dy == r);
+        const int step = face ? 1 : 2 * r;
+        for (int dx = -r; dx <= r; dx += (step > 0 ? step : 1)) {
+          const int x = c[0] + dx;
+          if (x < 0 || x >= G.g[0]) continue;
+          // box lower bound (cell grown by delta)
+          const int cc[3] = {x, y, z};
+          double bd2 = 0.0;
+#pragma unroll
+          for (int a = 0; a < 3; ++a) {
+            const double lo = G.o[a] + cc[a] * G.h - G.delta;
+            const double hi = G.o[a] + (cc[a] + 1) * G.h + G.delta;
+            const double e = fmax(0.0, fmax(lo - qv[a], qv[a] - hi));
+            bd2 += e * e;
+          }
+          if (bd2 > thr) continue;
+          const int cell = (z * G.g[1] + y) * G.g[0] + x;
+          const int b = start[cell], e = b + cnt[cell];
+          for (int t = b; t < e; ++t) {
+            const Rec rr = rec[t];
+            const double dx2 = rr.x - qx, dy2 = rr.y - qy, dz2 = rr.z - qz;
+            const double dsq = dx2 * dx2 + dy2 * dy2 + dz2 * dz2;
+            if (!(dsq <= thr)) continue;
+            const double d = __builtin_sqrt(dsq);
+            if (!knn_less(d, rr.idx, kd[K - 1], ki[K - 1])) continue;
+            bool placed = false;
+#pragma unroll
+            for (int s = K - 1; s >= 0; --s) {
+              if (!placed) {
+                if (s > 0 && knn_less(d, rr.idx, kd[s - 1], ki[s - 1])) {
+                  kd[s] = kd[s - 1];
+                  ki[s] = ki[s - 1];
+                } else {
+                  kd[s] = d;
+                  ki[s] = rr.idx;
+                  placed = true;
+                }
+              }
+            }
+            const double w = kd[K - 1];
+            thr = w < INFINITY ? w * w * (1.0 + 0x1p-48) : INFINITY;
+          }
+        }
+      }
+    }
+    // lower bound on any point outside the visited (2r+1)^3 block
+    double L = INFINITY;
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+      if (c[a] - r > 0) L = fmin(L, qv[a] - (G.o[a] + (c[a] - r) * G.h));
+      if (c[a] + r < G.g[a] - 1)
+        L = fmin(L, (G.o[a] + (c[a] + r + 1) * G.h) - qv[a]);
+    }
+    if (L == INFINITY) break;               // whole grid visited
+    if (kd[K - 1] < L - 2.0 * G.delta) break;  // k found, nothing closer left
+  }
+#pragma unroll
+  for (int s = 0; s < K; ++s) {
+    oidx[q * K + s] = ki[s];
+    odist[q * K + s] = kd[s];
+  }
+}
+
+}  // namespace
+
+// =================================================================== host
+struct navgpu_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  bool own_stream = false;
+  std::map<int, std::pair<void *, size_t>> bufs;  // grow-only workspace
+  bool timing = false;
+  std::map<std::string, std::vector<std::pair<hipEvent_t, hipEvent_t>>> ev;
+  std::vector<hipEvent_t> free_ev;
+  std::vector<double> tan_c, tan_r;
+  int tan_R = -1, tan_C = -1;
+};
+
+namespace {
+
+enum Slot {
+  kBBox = 1, kParams, kCnt, kStart, kBSum, kCellId, kSlotBuf, kRec, kTan,
+  kKdFc, kKdP, kKdT,
+  kH0 = 100, kH1, kH2, kH3, kH4, kH5,
+};
+
+int ws_get(navgpu_ctx *ctx, int slot, size_t bytes, void **out) {
+  auto &b = ctx->bufs[slot];
+  if (b.second < bytes || !b.first) {
+    if (b.first) {
+      HIP_TRY(hipStreamSynchronize(ctx->stream));
+      HIP_TRY(hipFree(b.first));
+      b.first = nullptr;
+      b.second = 0;
+    }
+    size_t want = bytes < 256 ? 256 : bytes;
+    hipError_t e = hipMalloc(&b.first, want);
+    if (e != hipSuccess) {
+      set_err("hipMalloc(%zu): %s", want, hipGetErrorString(e));
+      b.first = nullptr;
+      return NAVGPU_ENOMEM;
+    }
+    b.second = want;
+  }
+  *out = b.first;
+  return NAVGPU_OK;
+}
+
+template <class T>
+int ws(navgpu_ctx *ctx, int slot, size_t count, T **out) {
+  void *p;
+  int rc = ws_get(ctx, slot, count * sizeof(T), &p);
+  *out = (T *)p;
+  return rc;
+}
+
+#define RC(x)                    \
+  do {                           \
+    int rc_ = (x);               \
+    if (rc_ != NAVGPU_OK) return rc_; \
+  } while (0)
+
+struct TimedRegion {
+  navgpu_ctx *ctx;
+  const char *name;
+  hipEvent_t a = nullptr, b = nullptr;
+  hipEvent_t take() {
+    if (!ctx->free_ev.empty()) {
+      hipEvent_t e = ctx->free_ev.back();
+      ctx->free_ev.pop_back();
+      return e;
+    }
+    hipEvent_t e = nullptr;
+    if (hipEventCreate(&e) != hipSuccess) return nullptr;
+    return e;
+  }
+  TimedRegion(navgpu_ctx *c, const char *n) : ctx(c), name(n) {
+    if (!ctx->timing) return;
+    a = take();
+    b = take();
+    if (a && b) (void)hipEventRecord(a, ctx->stream);
+  }
+  ~TimedRegion() {
+    if (!ctx->timing || !a || !b) return;
+    (void)hipEventRecord(b, ctx->stream);
+    ctx->ev[name].push_back({a, b});
+  }
+};
+
+int lds_limit() {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return 65536;
+  int v = 0;
+  if (hipDeviceGetAttribute(&v, hipDeviceAttributeMaxSharedMemoryPerBlock,
+                            dev) != hipSuccess || v <= 0)
+    return 65536;
+  return v;
+}
+
+int check_rows_shape(int R, int C, bool stack) {
+  ARG_CHECK(R >= 0 && C >= 0);
+  if (C > kMaxRowCols) {
+    set_err("rows kernels: C=%d exceeds %d", C, kMaxRowCols);
+    return NAVGPU_ERANGE;
+  }
+  const RowsLds L = rows_lds(C, kRowsBlock, stack);
+  if (L.total > lds_limit()) {
+    set_err("rows kernels: C=%d needs %d B of LDS (device limit %d)", C,
+            L.total, lds_limit());
+    return NAVGPU_ERANGE;
+  }
+  return NAVGPU_OK;
+}
+
+template <class Kern>
+int set_lds(Kern k, int bytes) {
+  HIP_TRY(hipFuncSetAttribute((const void *)k,
+                              hipFuncAttributeMaxDynamicSharedMemorySize,
+                              bytes));
+  return NAVGPU_OK;
+}
+
+unsigned grid1d(size_t n, int block) {
+  return (unsigned)((n + block - 1) / block);
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------ C ABI
+extern "C" {
+
+const char *navgpu_last_error(void) { return g_err; }
+const char *navgpu_version(void) { return NAVGPU_VERSION; }
+
+int navgpu_create(int device, void *stream, navgpu_ctx **out) {
+  ARG_CHECK(out);
+  *out = nullptr;
+  int ndev = 0;
+  HIP_TRY(hipGetDeviceCount(&ndev));
+  if (device < 0 || device >= ndev) {
+    set_err("device %d not present (%d visible)", device, ndev);
+    return NAVGPU_EHIP;
+  }
+  hipDeviceProp_t prop;
+  HIP_TRY(hipGetDeviceProperties(&prop, device));
+  if (strncmp(prop.gcnArchName, "gfx950", 6) != 0) {
+    set_err("device %d is %s; libnavgpu is built for gfx950 (MI355X) only",
+            device, prop.gcnArchName);
+    return NAVGPU_EHIP;
+  }
+  HIP_TRY(hipSetDevice(device));
+  navgpu_ctx *c = new navgpu_ctx();
+  c->device = device;
+  if (stream) {
+    c->stream = (hipStream_t)stream;
+  } else {
+    hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+    if (e != hipSuccess) {
+      delete c;
+      set_err("hipStreamCreate: %s", hipGetErrorString(e));
+      return NAVGPU_EHIP;
+    }
+    c->own_stream = true;
+  }
+  *out = c;
+  return NAVGPU_OK;
+}
+
+void navgpu_destroy(navgpu_ctx *ctx) {
+  if (!ctx) return;
+  (void)hipSetDevice(ctx->device);
+  (void)hipStreamSynchronize(ctx->stream);
+  for (auto &kv : ctx->bufs)
+    if (kv.second.first) (void)hipFree(kv.second.first);
+  for (auto &kv : ctx->ev)
+    for (auto &pr : kv.second) {
+      (void)hipEventDestroy(pr.first);
+      (void)hipEventDestroy(pr.second);
+    }
+  for (auto e : ctx->free_ev) (void)hipEventDestroy(e);
+  if (ctx->own_stream) (void)hipStreamDestroy(ctx->stream);
+  delete ctx;
+}
+
+int navgpu_set_stream(navgpu_ctx *ctx, void *stream) {
+  ARG_CHECK(ctx && stream);
+  if (ctx->own_stream) {
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    HIP_TRY(hipStreamDestroy(ctx->stream));
+    ctx->own_stream = false;
+  }
+  ctx->stream = (hipStream_t)stream;
+  return NAVGPU_OK;
+}
+
+void *navgpu_stream(navgpu_ctx *ctx) { return ctx ? (void *)ctx->stream : nullptr; }
+
+int navgpu_sync(navgpu_ctx *ctx) {
+  ARG_CHECK(ctx);
+  HIP_TRY(hipStreamSynchronize(ctx->stream));
+  return NAVGPU_OK;
+}
+
+int navgpu_rows_max_cols(void) {
+  const int lim = lds_limit();
+  int lo = 0, hi = kMaxRowCols;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) / 2;
+    if (rows_lds(mid, kRowsBlock, true).total <= lim)
+      lo = mid;
+    else
+      hi = mid - 1;
+  }
+  return lo;
+}
+
+void navgpu_timing_enable(navgpu_ctx *ctx, int on) {
+  if (ctx) ctx->timing = on != 0;
+}
+
+double navgpu_timing_read(navgpu_ctx *ctx, const char *name, int reset) {
+  if (!ctx || !name) return -1.0;
+  auto it = ctx->ev.find(name);
+  if (it == ctx->ev.end()) return -1.0;
+  double ms = 0.0;
+  for (auto &pr : it->second) {
+    if (hipEventSynchronize(pr.second) != hipSuccess) return -1.0;
+    float t = 0.f;
+    if (hipEventElapsedTime(&t, pr.first, pr.second) != hipSuccess) return -1.0;
+    ms += t;
+  }
+  if (reset) {
+    for (auto &pr : it->second) {
+      ctx->free_ev.push_back(pr.first);
+      ctx->free_ev.push_back(pr.second);
+    }
+    it->second.clear();
+  }
+  return ms;
+}
+
+int navgpu_timing_count(navgpu_ctx *ctx, const char *name) {
+  if (!ctx || !name) return -1;
+  auto it = ctx->ev.find(name);
+  return it == ctx->ev.end() ? 0 : (int)it->second.size();
+}
+
+// ---------------------------------------------------------------- R1
+int navgpu_curvature_dev(navgpu_ctx *ctx, const double *pts, int R, int C,
+                         int32_t *mask, double *curv) {
+  ARG_CHECK(ctx && R >= 0 && C >= 0);
+  if ((size_t)R * C == 0) return NAVGPU_OK;
+  ARG_CHECK(pts && mask);
+  TimedRegion tr(ctx, "curvature");
+  dim3 grid((C + kCurvTile - 1) / kCurvTile, R);
+  hipLaunchKernelGGL(k_curvature, grid, dim3(kCurvTile), 0, ctx->stream, pts,
+                     R, C, mask, curv);
+  CHECK_LAUNCH("k_curvature");
+  return NAVGPU_OK;
+}
+
+int navgpu_curvature_host(navgpu_ctx *ctx, const double *pts, int R, int C,
+                          int32_t *mask, double *curv) {
+  ARG_CHECK(ctx && R >= 0 && C >= 0);
+  const size_t N = (size_t)R * C;
+  if (!N) return NAVGPU_OK;
+  ARG_CHECK(pts && mask);
+  double *dp, *dc = nullptr;
+  int32_t *dm;
+  RC(ws(ctx, kH0, 3 * N, &dp));
+  RC(ws(ctx, kH1, N, &dm));
+  if (curv) RC(ws(ctx, kH2, N, &dc));
+  HIP_TRY(hipMemcpyAsync(dp, pts, 24 * N, hipMemcpyHostToDevice, ctx->stream));
+  RC(navgpu_curvature_dev(ctx, dp, R, C, dm, dc));
+  HIP_TRY(hipMemcpyAsync(mask, dm, 4 * N, hipMemcpyDeviceToHost, ctx->stream));
+  if (curv)
+    HIP_TRY(hipMemcpyAsync(curv, dc, 8 * N, hipMemcpyDeviceToHost, ctx->stream));
+  HIP_TRY(hipStreamSynchronize(ctx->stream));
+  return NAVGPU_OK;
+}
+
+// ---------------------------------------------------------------- R2
+int navgpu_project_dev(navgpu_ctx *ctx, const int32_t *depth, int R, int C,
+                       double *pts) {
+  ARG_CHECK(ctx && R >= 0 && C >= 0);
+  const size_t N = (size_t)R * C;
+  if (!N) return NAVGPU_OK;
+  ARG_CHECK(depth && pts);
+  double *dt;
+  RC(ws(ctx, kTan, (size_t)R + C, &dt));
+  if (ctx->tan_R != R || ctx->tan_C != C) {
+    // utils/pointcloud.c:10-36, the angle tables with the host's libm tan
+    const double fov_h = 45.0, fov_v = 45.0;
+    const double theta_step_deg = fov_h / (C - 1);
+    const double phi_step_deg = fov_v / (R - 1);
+    ctx->tan_c.resize(C);
+    ctx->tan_r.resize(R);
+    for (int i = 0; i < C; ++i) {
+      double theta = -fov_h / 2.0 + i * theta_step_deg;
+      theta = theta * M_PI / 180.0;
+      ctx->tan_c[i] = tan(theta);
+    }
+    for (int j = 0; j < R; ++j) {
+      double phi = -fov_v / 2.0 + j * phi_step_deg;
+      phi = phi * M_PI / 180.0;
+      ctx->tan_r[j] = tan(phi);
+    }
+    HIP_TRY(hipMemcpyAsync(dt, ctx->tan_c.data(), 8 * (size_t)C,
+                           hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(hipMemcpyAsync(dt + C, ctx->tan_r.data(), 8 * (size_t)R,
+                           hipMemcpyHostToDevice, ctx->stream));
+    ctx->tan_R = R;
+    ctx->tan_C = C;
+  }
+  hipLaunchKernelGGL(k_project, dim3(grid1d(N, 256)), dim3(256), 0,
+                     ctx->stream, depth, R, C, dt, dt + C, pts);
+  CHECK_LAUNCH("k_project");
+  return NAVGPU_OK;
+}
+
+int navgpu_project_host(navgpu_ctx *ctx, const int32_t *depth, int R, int C,
+                        double *pts) {
+  ARG_CHECK(ctx && R >= 0 && C >= 0);
+  const size_t N = (size_t)R * C;
+  if (!N) return NAVGPU_OK;
+  ARG_CHECK(depth && pts);
+  int32_t *dd;
+  double *dp;
+  RC(ws(ctx, kH0, N, &dd));
+  RC(ws(ctx, kH1, 3 * N, &dp));
+  HIP_TRY(hipMemcpyAsync(dd, depth, 4 * N, hipMemcpyHostToDevice, ctx->stream));
+  RC(navgpu_project_dev(ctx, dd, R, C, dp));
+  HIP_TRY(hipMemcpyAsync(pts, dp, 24 * N, hipMemcpyDeviceToHost, ctx->stream));
+  HIP_TRY(hipStreamSynchronize(ctx->stream));
+  return NAVGPU_OK;
+}
+
+// ---------------------------------------------------------------- R3
+int navgpu_transform_dev(navgpu_ctx *ctx, const double *pts, size_t n,
+                         const double Rm[9], const double t[3],
+                         const double tr[3], double *out, double *out_last) {
+  ARG_CHECK(ctx);
+  if (!n) return NAVGPU_OK;
+  ARG_CHECK(pts && Rm && t && out);
+  ARG_CHECK(!out_last || tr);
+  Rigid g;
+  memcpy(g.R, Rm, sizeof(g.R));
+  memcpy(g.t, t, sizeof(g.t));
+  if (tr)
+    memcpy(g.tr, tr, sizeof(g.tr));
+  else
+    memset(g.tr, 0, sizeof(g.tr));
+  hipLaunchKernelGGL(k_transform, dim3(grid1d(n, 256)), dim3(256), 0,
+                     ctx->stream, pts, n, g, out, out_last);
+  CHECK_LAUNCH("k_transform");
+  return NAVGPU_OK;
+}
+
+// ------------------------------------------------------------ R4-R6 rows
+int navgpu_kd_build_rows_dev(navgpu_ctx *ctx, const double *feat_src,
+                             const double *coords, int R, int C,
+                             double *tree_pts, int32_t *tree_col,
+                             int32_t *tree_n, int32_t *mask_out) {
+  ARG_CHECK(ctx);
+  RC(check_rows_shape(R, C, false));
+  if (R == 0) return NAVGPU_OK;
+  ARG_CHECK(tree_n);
+  if (C == 0) {
+    HIP_TRY(hipMemsetAsync(tree_n, 0, 4 * (size_t)R, ctx->stream));
+    return NAVGPU_OK;
+  }
+  ARG_CHECK(feat_src && coords && tree_pts && tree_col);
+  const RowsLds L = rows_lds(C, kRowsBlock, false);
+  RC(set_lds(k_rows_build, L.total));
+  TimedRegion tr(ctx, "rows_build");
+  hipLaunchKernelGGL(k_rows_build, dim3(R), dim3(kRowsBlock), L.total,
+                     ctx->stream, feat_src, coords, R, C, tree_pts, tree_col,
+                     tree_n, mask_out);
+  CHECK_LAUNCH("k_rows_build");
+  return NAVGPU_OK;
+}
+
+int navgpu_kd_query_rows_dev(navgpu_ctx *ctx, const double *tree_pts,
+                             const int32_t *tree_n, const double *feat_src,
+                             const double *queries, int R, int C,
+                             int32_t *nn_pos, double *nn_dist,
+                             int32_t *mask_out) {
+  ARG_CHECK(ctx);
+  RC(check_rows_shape(R, C, true));
+  if ((size_t)R * C == 0) return NAVGPU_OK;
+  ARG_CHECK(tree_pts && tree_n && feat_src && queries && nn_pos && nn_dist);
+  const RowsLds L = rows_lds(C, kRowsBlock, true);
+  RC(set_lds(k_rows_query, L.total));
+  TimedRegion tr(ctx, "rows_query");
+  hipLaunchKernelGGL(k_rows_query, dim3(R), dim3(kRowsBlock), L.total,
+                     ctx->stream, tree_pts, tree_n, feat_src, queries, R, C,
+                     nn_pos, nn_dist, mask_out);
+  CHECK_LAUNCH("k_rows_query");
+  return NAVGPU_OK;
+}
+
+int navgpu_rows_match_dev(navgpu_ctx *ctx, const double *src,
+                          const double *tgt, int R, int C, int32_t *src_mask,
+                          int32_t *tgt_mask, int32_t *nn_idx, double *nn_dist) {
+  ARG_CHECK(ctx);
+  RC(check_rows_shape(R, C, true));
+  if ((size_t)R * C == 0) return NAVGPU_OK;
+  ARG_CHECK(src && tgt && nn_idx && nn_dist);
+  const RowsLds L = rows_lds(C, kRowsBlock, true);
+  RC(set_lds(k_rows_match, L.total));
+  TimedRegion tr(ctx, "rows_match");
+  hipLaunchKernelGGL(k_rows_match, dim3(R), dim3(kRowsBlock), L.total,
+                     ctx->stream, src, tgt, R, C, src_mask, tgt_mask, nn_idx,
+                     nn_dist);
+  CHECK_LAUNCH("k_rows_match");
+  return NAVGPU_OK;
+}
+
+int navgpu_rows_match_host(navgpu_ctx *ctx, const double *src,
+                           const double *tgt, int R, int C, int32_t *src_mask,
+                           int32_t *tgt_mask, int32_t *nn_idx,
+                           double *nn_dist) {
+  ARG_CHECK(ctx && R >= 0 && C >= 0);
+  const size_t N = (size_t)R * C;
+  if (!N) return NAVGPU_OK;
+  ARG_CHECK(src && tgt && nn_idx && nn_dist);
+  double *ds, *dt, *dd;
+  int32_t *dsm, *dtm, *di;
+  RC(ws(ctx, kH0, 3 * N, &ds));
+  RC(ws(ctx, kH1, 3 * N, &dt));
+  RC(ws(ctx, kH2, N, &dsm));
+  RC(ws(ctx, kH3, N, &dtm));
+  RC(ws(ctx, kH4, N, &di));
+  RC(ws(ctx, kH5, N, &dd));
+  HIP_TRY(hipMemcpyAsync(ds, src, 24 * N, hipMemcpyHostToDevice, ctx->stream));
+  HIP_TRY(hipMemcpyAsync(dt, tgt, 24 * N, hipMemcpyHostToDevice, ctx->stream));
+  RC(navgpu_rows_match_dev(ctx, ds, dt, R, C, dsm, dtm, di, dd));
+  HIP_TRY(hipMemcpyAsync(nn_idx, di, 4 * N, hipMemcpyDeviceToHost, ctx->stream));
+  HIP_TRY(hipMemcpyAsync(nn_dist, dd, 8 * N, hipMemcpyDeviceToHost, ctx->stream));
+  if (src_mask)
+    HIP_TRY(hipMemcpyAsync(src_mask, dsm, 4 * N, hipMemcpyDeviceToHost, ctx->stream));
+  if (tgt_mask)
+    HIP_TRY(hipMemcpyAsync(tgt_mask, dtm, 4 * N, hipMemcpyDeviceToHost, ctx->stream));
+  HIP_TRY(hipStreamSynchronize(ctx->stream));
+  return NAVGPU_OK;
+}
+
+// ------------------------------------------------- kdtree.h buildKDTree
+int navgpu_kd_build_dev(navgpu_ctx *ctx, double *pts, size_t n, int depth0) {
+  ARG_CHECK(ctx && depth0 >= 0);
+  ARG_CHECK(n < ((size_t)1 << 30));
+  if (n < 2) return NAVGPU_OK;  // kdtree.c:22: nothing to permute
+  ARG_CHECK(pts);
+  const int ni = (int)n;
+  TimedRegion tr(ctx, "kd_build");
+  if (n <= 65535 && kd_build_lds_bytes(ni) <= lds_limit()) {
+    const int lds = kd_build_lds_bytes(ni);
+    RC(set_lds(k_kd_build_lds, lds));
+    hipLaunchKernelGGL(k_kd_build_lds, dim3(1), dim3(1024), lds, ctx->stream,
+                       pts, ni, depth0 % 3);
+    CHECK_LAUNCH("k_kd_build_lds");
+    return NAVGPU_OK;
+  }
+  double *fc;
+  uint32_t *P, *T;
+  RC(ws(ctx, kKdFc, 3 * n, &fc));
+  RC(ws(ctx, kKdP, n, &P));
+  RC(ws(ctx, kKdT, n, &T));
+  hipLaunchKernelGGL(k_kd_build_global, dim3(1), dim3(1024), 0, ctx->stream,
+                     pts, ni, depth0 % 3, fc, P, T);
+  CHECK_LAUNCH("k_kd_build_global");
+  return NAVGPU_OK;
+}
+
+int navgpu_kd_build_host(navgpu_ctx *ctx, double *pts, size_t n, int depth0) {
+  ARG_CHECK(ctx);
+  if (n < 2) return NAVGPU_OK;
+  ARG_CHECK(pts);
+  double *dp;
+  RC(ws(ctx, kH0, 3 * n, &dp));
+  HIP_TRY(hipMemcpyAsync(dp, pts, 24 * n, hipMemcpyHostToDevice, ctx->stream));
+  RC(navgpu_kd_build_dev(ctx, dp, n, depth0));
+  HIP_TRY(hipMemcpyAsync(pts, dp, 24 * n, hipMemcpyDeviceToHost, ctx->stream));
+  HIP_TRY(hipStreamSynchronize(ctx->stream));
+  return NAVGPU_OK;
+}
+
+// ------------------------------------------------------ memory helpers
+int navgpu_malloc(navgpu_ctx *ctx, size_t bytes, void **dptr) {
+  ARG_CHECK(ctx && dptr);
+  *dptr = nullptr;
+  hipError_t e = hipMalloc(dptr, bytes ? bytes : 16);
+  if (e != hipSuccess) {
+    set_err("hipMalloc(%zu): %s", bytes, hipGetErrorString(e));
+    *dptr = nullptr;
+    return NAVGPU_ENOMEM;
+  }
+  return NAVGPU_OK;
+}
+
+void navgpu_free(navgpu_ctx *ctx, void *dptr) {
+  if (!ctx || !dptr) return;
+  (void)hipStreamSynchronize(ctx->stream);
+  (void)hipFree(dptr);
+}
+
+int navgpu_upload(navgpu_ctx *ctx, void *dst, const void *src, size_t bytes) {
+  ARG_CHECK(ctx);
+  if (!bytes) return NAVGPU_OK;
+  ARG_CHECK(dst && src);
+  HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, ctx->stream));
+  return NAVGPU_OK;
+}
+
+int navgpu_download(navgpu_ctx *ctx, void *dst, const void *src, size_t bytes) {
+  ARG_CHECK(ctx);
+  if (!bytes) return NAVGPU_OK;
+  ARG_CHECK(dst && src);
+  HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, ctx->stream));
+  return NAVGPU_OK;
+}
+
+// ------------------------------------------------------------ global k-NN
+int navgpu_knn_dev(navgpu_ctx *ctx, const double *tgt, size_t nt,
+                   const double *queries, size_t nq, int k, int32_t *idx,
+                   double *dist) {
+  ARG_CHECK(ctx && k >= 1 && k <= 16);
+  ARG_CHECK(nt < (size_t)INT32_MAX && nq < ((size_t)1 << 40));
+  if (!nq) return NAVGPU_OK;
+  ARG_CHECK(queries && idx && dist && (tgt || nt == 0));
+  const int cap = (int)(nt / kOcc) * 2 + 1024;
+  unsigned long long *bbox;
+  GridParams *gp;
+  int *cnt, *start, *bsum, *cellid = nullptr, *slot = nullptr;
+  Rec *rec = nullptr;
+  RC(ws(ctx, kBBox, 6, &bbox));
+  RC(ws(ctx, kParams, 1, &gp));
+  RC(ws(ctx, kCnt, cap, &cnt));
+  RC(ws(ctx, kStart, cap, &start));
+  const int nb = (cap + kScanTile - 1) / kScanTile;
+  if (nb > kScanTile) {
+    set_err("knn: %zu targets exceed the scan capacity", nt);
+    return NAVGPU_ERANGE;
+  }
+  RC(ws(ctx, kBSum, nb, &bsum));
+  if (nt) {
+    RC(ws(ctx, kCellId, nt, &cellid));
+    RC(ws(ctx, kSlotBuf, nt, &slot));
+    RC(ws(ctx, kRec, nt, &rec));
+  }
+  hipStream_t s = ctx->stream;
+  HIP_TRY(hipMemsetAsync(bbox, 0xff, 24, s));
+  HIP_TRY(hipMemsetAsync(bbox + 3, 0x00, 24, s));
+  HIP_TRY(hipMemsetAsync(cnt, 0, 4 * (size_t)cap, s));
+  if (nt) {
+    const unsigned gb = (unsigned)std::min<size_t>(grid1d(nt, 256), 2048);
+    hipLaunchKernelGGL(k_bbox, dim3(gb), dim3(256), 0, s, tgt, nt, bbox);
+    CHECK_LAUNCH("k_bbox");
+  }
+  hipLaunchKernelGGL(k_grid_params, dim3(1), dim3(64), 0, s, bbox, nt, cap, gp);
+  CHECK_LAUNCH("k_grid_params");
+  if (nt) {
+    hipLaunchKernelGGL(k_cell_count, dim3(grid1d(nt, 256)), dim3(256), 0, s,
+                       tgt, nt, gp, cnt, cellid, slot);
+    CHECK_LAUNCH("k_cell_count");
+  }
+  hipLaunchKernelGGL(k_scan_sums, dim3(nb), dim3(kScanBlock), 0, s, cnt, cap, bsum);
+  CHECK_LAUNCH("k_scan_sums");
+  hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(kScanBlock), 0, s, bsum, nb);
+  CHECK_LAUNCH("k_scan_top");
+  hipLaunchKernelGGL(k_scan_apply, dim3(nb), dim3(kScanBlock), 0, s, cnt, cap,
+                     bsum, start);
+  CHECK_LAUNCH("k_scan_apply");
+  if (nt) {
+    hipLaunchKernelGGL(k_scatter, dim3(grid1d(nt, 256)), dim3(256), 0, s, tgt,
+                       nt, cellid, slot, start, rec);
+    CHECK_LAUNCH("k_scatter");
+  }
+  TimedRegion tr(ctx, "knn_query");
+  const dim3 g(grid1d(nq, 256)), b(256);
+#define KNN_CASE(KK)                                                         \
+  case KK:                                                                   \
+    hipLaunchKernelGGL(k_knn<KK>, g, b, 0, s, gp, start, cnt, rec, queries, \
+                       nq, idx, dist);                                       \
+    break;
+  switch (k) {
+    KNN_CASE(1)
+    KNN_CASE(2)
+    KNN_CASE(3)
+    KNN_CASE(4)
+    KNN_CASE(5)
+    KNN_CASE(6)
+    KNN_CASE(7)
+    KNN_CASE(8)
+    KNN_CASE(9)
+    KNN_CASE(10)
+    KNN_CASE(11)
+    KNN_CASE(12)
+    KNN_CASE(13)
+    KNN_CASE(14)
+    KNN_CASE(15)
+    KNN_CASE(16)
+  }
+#undef KNN_CASE
+  CHECK_LAUNCH("k_knn");
+  return NAVGPU_OK;
+}
+
+int navgpu_knn_host(navgpu_ctx *ctx, const double *tgt, size_t nt,
+                    const double *queries, size_t nq, int k, int32_t *idx,
+                    double *dist) {
+  ARG_CHECK(ctx && k >= 1 && k <= 16);
+  if (!nq) return NAVGPU_OK;
+  ARG_CHECK(queries && idx && dist && (tgt || nt == 0));
+  double *dt = nullptr, *dq, *dd;
+  int32_t *di;
+  if (nt) RC(ws(ctx, kH0, 3 * nt, &dt));
+  RC(ws(ctx, kH1, 3 * nq, &dq));
+  RC(ws(ctx, kH2, nq * k, &di));
+  RC(ws(ctx, kH3, nq * k, &dd));
+  if (nt)
+    HIP_TRY(hipMemcpyAsync(dt, tgt, 24 * nt, hipMemcpyHostToDevice, ctx->stream));
+  HIP_TRY(hipMemcpyAsync(dq, queries, 24 * nq, hipMemcpyHostToDevice, ctx->stream));
+  RC(navgpu_knn_dev(ctx, dt, nt, dq, nq, k, di, dd));
+  HIP_TRY(hipMemcpyAsync(idx, di, 4 * nq * k, hipMemcpyDeviceToHost, ctx->stream));
+  HIP_TRY(hipMemcpyAsync(dist, dd, 8 * nq * k, hipMemcpyDeviceToHost, ctx->stream));
+  HIP_TRY(hipStreamSynchronize(ctx->stream));
+  return NAVGPU_OK;
+}
+
+int navgpu_pair_knn_dev(navgpu_ctx *ctx, const double *src, const double *tgt,
+                        int R, int C, int k, int32_t *src_mask,
+                        int32_t *tgt_mask, int32_t *idx, double *dist) {
+  ARG_CHECK(ctx && R >= 0 && C >= 0);
+  const size_t N = (size_t)R * C;
+  if (!N) return NAVGPU_OK;
+  if (src_mask) RC(navgpu_curvature_dev(ctx, src, R, C, src_mask, nullptr));
+  if (tgt_mask) RC(navgpu_curvature_dev(ctx, tgt, R, C, tgt_mask, nullptr));
+  return navgpu_knn_dev(ctx, tgt, N, src, N, k, idx, dist);
+}
+
+}  // extern "C"

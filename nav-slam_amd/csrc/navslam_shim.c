@@ -1,0 +1,512 @@
+/*
+ * navslam_shim.c — the drop-in C ABI of NAV-SLAM's scan-matching path:
+ * slam.h (init_slam / slam_localization / slam_mapping), kdtree.h
+ * (buildKDTree / freeKDTree / nearestNeighborSearch / printKDTree),
+ * pointcloud.h (convertToPointCloud / printPointCloud) and slam.c's
+ * extract_feature, implemented over libnavgpu (include/navgpu.h).
+ *
+ * Built once per grid size (libnavslam_<R>x<C>.so, -DMAX_ROWS/-DMAX_COLS),
+ * because the reference's structs embed the dims. src/main.c and src/ekf.c
+ * link against it unchanged.
+ *
+ * What runs where, per frame:
+ *   GPU : rigid transform (src/slam.c:145-160,193-210,402-416), curvature
+ *         (src/slam.c:11-61), per-row feature compaction + the reference's
+ *         exact KD permutation (src/slam.c:64-81, utils/kdtree.c:20-82), and
+ *         the per-feature 1-NN batch (src/slam.c:236-244, utils/kdtree.c:
+ *         110-152).
+ *   host: the correspondence dedup and the 3-DOF Adam loop
+ *         (src/slam.c:247-389): a sequential floating-point sum whose
+ *         rounding order is part of the result, kept bit-identical here
+ *         (dedup by hash instead of the reference's O(F^2) scan, same
+ *         first-insertion order and keep-smaller-distance rule).
+ * There is no CPU fallback for the GPU part: a device failure prints the
+ * error and aborts (the reference API has no status codes).
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "navgpu.h"
+#include "slam.h"
+
+#define ROWS MAX_ROWS
+#define COLS MAX_COLS
+#define NPTS ((size_t)MAX_ROWS * MAX_COLS)
+#define DEG2RAD(x) ((x) * M_PI / 180.0) /* src/slam.c:8 */
+
+/* ----------------------------------------------------------- context */
+static navgpu_ctx *g_ctx;
+
+static void die(const char *what, int rc)
+{
+    fprintf(stderr, "navslam: %s failed (%d): %s\n", what, rc,
+            navgpu_last_error());
+    abort();
+}
+
+#define CK(x)                        \
+    do {                             \
+        int rc_ = (x);               \
+        if (rc_ != NAVGPU_OK)        \
+            die(#x, rc_);            \
+    } while (0)
+
+static navgpu_ctx *ctx(void)
+{
+    if (!g_ctx) {
+        const char *d = getenv("NAVSLAM_DEVICE");
+        CK(navgpu_create(d ? atoi(d) : 0, NULL, &g_ctx));
+    }
+    return g_ctx;
+}
+
+static int quiet(void)
+{
+    const char *q = getenv("NAVSLAM_QUIET");
+    return q && *q && *q != '0';
+}
+
+static int host_trees(void)
+{
+    const char *q = getenv("NAVSLAM_HOST_TREES");
+    return !(q && *q == '0');
+}
+
+/* ------------------------------------- host KDNode blocks + registry */
+/* Every tree this library hands out is one malloc'd block of KDNode laid
+ * out in the implicit order (node of [lo,hi) at lo+(hi-lo)/2), linked like
+ * the reference's per-node mallocs. freeKDTree recognises block roots. */
+typedef struct {
+    KDNode *root, *base;
+    size_t n;
+} kd_block;
+static kd_block *g_blocks;
+static size_t g_nblocks, g_capblocks;
+
+static KDNode *link_range(KDNode *b, const Point *pts, size_t lo, size_t hi)
+{
+    if (lo >= hi)
+        return NULL;
+    size_t mid = lo + (hi - lo) / 2;
+    KDNode *nd = &b[mid];
+    nd->point = pts[mid];
+    nd->left = link_range(b, pts, lo, mid);
+    nd->right = link_range(b, pts, mid + 1, hi);
+    return nd;
+}
+
+static KDNode *make_block(const Point *pts, size_t n)
+{
+    if (n == 0)
+        return NULL;
+    KDNode *b = malloc(sizeof(KDNode) * n);
+    if (!b) {
+        fprintf(stderr, "navslam: out of host memory\n");
+        abort();
+    }
+    KDNode *root = link_range(b, pts, 0, n);
+    if (g_nblocks == g_capblocks) {
+        g_capblocks = g_capblocks ? 2 * g_capblocks : 64;
+        g_blocks = realloc(g_blocks, sizeof(kd_block) * g_capblocks);
+    }
+    g_blocks[g_nblocks].root = root;
+    g_blocks[g_nblocks].base = b;
+    g_blocks[g_nblocks].n = n;
+    g_nblocks++;
+    return root;
+}
+
+static int release_block(KDNode *root)
+{
+    for (size_t i = g_nblocks; i-- > 0;) {
+        if (g_blocks[i].root == root) {
+            free(g_blocks[i].base);
+            g_blocks[i] = g_blocks[--g_nblocks];
+            return 1;
+        }
+    }
+    return 0;
+}
+
+/* utils/kdtree.c:84-91 */
+void freeKDTree(KDNode *root)
+{
+    if (!root)
+        return;
+    if (release_block(root))
+        return;
+    /* a subtree of one of our blocks: freed with its block's root */
+    for (size_t i = 0; i < g_nblocks; i++)
+        if (root >= g_blocks[i].base && root < g_blocks[i].base + g_blocks[i].n)
+            return;
+    /* a tree the caller built node by node with malloc */
+    freeKDTree(root->left);
+    freeKDTree(root->right);
+    free(root);
+}
+
+/* utils/kdtree.c:65-82 — the permutation is computed on the GPU. */
+KDNode *buildKDTree(Point *points, size_t numPoints, int depth)
+{
+    if (numPoints == 0)
+        return NULL;
+    CK(navgpu_kd_build_host(ctx(), (double *)points, numPoints, depth));
+    return make_block(points, numPoints);
+}
+
+/* utils/kdtree.c:94-107 */
+void printKDTree(KDNode *node, int depth)
+{
+    if (node == NULL)
+        return;
+    printf("\xe6\xb7\xb1\xe5\xba\xa6 %d: Point(x=%.2f, y=%.2f, z=%.2f)\n", depth,
+           node->point.x, node->point.y, node->point.z);
+    printKDTree(node->left, depth + 1);
+    printKDTree(node->right, depth + 1);
+}
+
+/* utils/kdtree.c:110-152 — one query against a linked host tree. */
+void nearestNeighborSearch(KDNode *root, Point *target, Point *result,
+                           double *bestDist, int depth)
+{
+    if (root == NULL)
+        return;
+    double dx = root->point.x - target->x;
+    double dy = root->point.y - target->y;
+    double dz = root->point.z - target->z;
+    double dist = sqrt(dx * dx + dy * dy + dz * dz);
+    if (dist < *bestDist) {
+        *bestDist = dist;
+        *result = root->point;
+    }
+    int axis = depth % 3;
+    double t = axis == 0 ? target->x : axis == 1 ? target->y : target->z;
+    double n = axis == 0 ? root->point.x : axis == 1 ? root->point.y
+                                                     : root->point.z;
+    KDNode *near = t < n ? root->left : root->right;
+    KDNode *far = t < n ? root->right : root->left;
+    nearestNeighborSearch(near, target, result, bestDist, depth + 1);
+    if (fabs(t - n) < *bestDist)
+        nearestNeighborSearch(far, target, result, bestDist, depth + 1);
+}
+
+/* --------------------------------------------------------- pointcloud.h */
+void convertToPointCloud(int distances[MAX_ROWS][MAX_COLS],
+                         Point pointCloud[MAX_ROWS][MAX_COLS])
+{
+    CK(navgpu_project_host(ctx(), (const int32_t *)&distances[0][0], ROWS,
+                           COLS, &pointCloud[0][0].x));
+}
+
+void printPointCloud(PointCloud pointcloud) /* utils/pointcloud.c:50-58 */
+{
+    for (int i = 0; i < MAX_ROWS; i++)
+        for (int j = 0; j < MAX_COLS; j++) {
+            Point p = pointcloud.ToF_position[i][j];
+            printf("point %d: (%f, %f, %f) \n", i * MAX_ROWS + j, p.x, p.y, p.z);
+        }
+}
+
+/* src/slam.c:11-61 — writes 1 where the reference does, leaves the rest. */
+void extract_feature(PointCloud *lidarPointCloud,
+                     int feature[MAX_ROWS][MAX_COLS])
+{
+    static int32_t mask[MAX_ROWS][MAX_COLS];
+    CK(navgpu_curvature_host(ctx(), &lidarPointCloud->ToF_position[0][0].x,
+                             ROWS, COLS, &mask[0][0], NULL));
+    for (int i = 0; i < ROWS; i++)
+        for (int j = 0; j < COLS; j++)
+            if (mask[i][j])
+                feature[i][j] = 1;
+}
+
+/* ------------------------------------------------ SLAM_attr side table */
+typedef struct {
+    SLAM_attr *key;
+    double *d_lidar, *d_global, *d_last, *d_tree, *d_dist;
+    int32_t *d_tcol, *d_tn, *d_pos;
+    int have_trees;
+    double h_tree[NPTS * 3];
+    int32_t h_tn[ROWS];
+    KDNode *roots[ROWS];
+    /* localisation scratch */
+    double h_tp[NPTS * 3];
+    double h_dist[NPTS];
+    int32_t h_pos[NPTS];
+} slam_state;
+
+static slam_state **g_states;
+static int g_nstates;
+
+static slam_state *state_for(SLAM_attr *a)
+{
+    for (int i = 0; i < g_nstates; i++)
+        if (g_states[i]->key == a)
+            return g_states[i];
+    slam_state *s = calloc(1, sizeof(*s));
+    if (!s) {
+        fprintf(stderr, "navslam: out of host memory\n");
+        abort();
+    }
+    s->key = a;
+    navgpu_ctx *c = ctx();
+    CK(navgpu_malloc(c, 24 * NPTS, (void **)&s->d_lidar));
+    CK(navgpu_malloc(c, 24 * NPTS, (void **)&s->d_global));
+    CK(navgpu_malloc(c, 24 * NPTS, (void **)&s->d_last));
+    CK(navgpu_malloc(c, 24 * NPTS, (void **)&s->d_tree));
+    CK(navgpu_malloc(c, 8 * NPTS, (void **)&s->d_dist));
+    CK(navgpu_malloc(c, 4 * NPTS, (void **)&s->d_tcol));
+    CK(navgpu_malloc(c, 4 * ROWS, (void **)&s->d_tn));
+    CK(navgpu_malloc(c, 4 * NPTS, (void **)&s->d_pos));
+    g_states = realloc(g_states, sizeof(*g_states) * (g_nstates + 1));
+    g_states[g_nstates++] = s;
+    return s;
+}
+
+/* src/slam.c:95-115 with the DEG2RAD of the callers */
+static void rotation(double roll, double pitch, double yaw, double R[9])
+{
+    double cr = cos(DEG2RAD(roll)), sr = sin(DEG2RAD(roll));
+    double cp = cos(DEG2RAD(pitch)), sp = sin(DEG2RAD(pitch));
+    double cy = cos(DEG2RAD(yaw)), sy = sin(DEG2RAD(yaw));
+    R[0] = cy * cp;
+    R[1] = cy * sp * sr - sy * cr;
+    R[2] = cy * sp * cr + sy * sr;
+    R[3] = sy * cp;
+    R[4] = sy * sp * sr + cy * cr;
+    R[5] = sy * sp * cr - cy * sr;
+    R[6] = -sp;
+    R[7] = cp * sr;
+    R[8] = cp * cr;
+}
+
+/* src/slam.c:143-172 / 395-427: global frame into the map slot, trees of
+ * the lidar-frame features over the global coordinates. */
+static void map_frame(SLAM_attr *attr, slam_state *s, Pos pos,
+                      PointCloud *lidar, int slot)
+{
+    navgpu_ctx *c = ctx();
+    double R[9], t[3] = {pos.x, pos.y, pos.z};
+    rotation(pos.roll, pos.pitch, pos.yaw, R);
+    attr->globalPointCloud[slot].ToF_timestamps = lidar->ToF_timestamps;
+    CK(navgpu_upload(c, s->d_lidar, &lidar->ToF_position[0][0], 24 * NPTS));
+    CK(navgpu_transform_dev(c, s->d_lidar, NPTS, R, t, NULL, s->d_global, NULL));
+    CK(navgpu_kd_build_rows_dev(c, s->d_lidar, s->d_global, ROWS, COLS,
+                                s->d_tree, s->d_tcol, s->d_tn, NULL));
+    CK(navgpu_download(c, &attr->globalPointCloud[slot].ToF_position[0][0],
+                       s->d_global, 24 * NPTS));
+    CK(navgpu_download(c, s->h_tree, s->d_tree, 24 * NPTS));
+    CK(navgpu_download(c, s->h_tn, s->d_tn, 4 * ROWS));
+    CK(navgpu_sync(c));
+    s->have_trees = 1;
+    int ht = host_trees();
+    for (int r = 0; r < ROWS; r++) {
+        if (s->roots[r])
+            freeKDTree(s->roots[r]); /* the reference leaks these */
+        s->roots[r] = ht ? make_block((const Point *)(s->h_tree + 3 * (size_t)r * COLS),
+                                      (size_t)s->h_tn[r])
+                         : NULL;
+        attr->kdtree_lastframe[r] = s->roots[r];
+    }
+}
+
+void init_slam(SLAM_attr *attr, Pos pos, PointCloud *lidarPointCloud)
+{
+    slam_state *s = state_for(attr);
+    attr->frameCount = 0;
+    attr->error = 0.0;
+    memset(s->roots, 0, sizeof(s->roots)); /* attr may be fresh stack memory */
+    map_frame(attr, s, pos, lidarPointCloud, 0);
+    attr->frameCount++;
+}
+
+void slam_mapping(SLAM_attr *attr, Pos pos, PointCloud *lidarPointCloud)
+{
+    slam_state *s = state_for(attr);
+    /* the reference writes globalPointCloud[frameCount] with no bound
+     * (src/slam.c:395); past SLAM_MAP_FRAMES the map is a ring here */
+    map_frame(attr, s, pos, lidarPointCloud, attr->frameCount % SLAM_MAP_FRAMES);
+    attr->frameCount++;
+}
+
+/* correspondence list entry: NeighborResult (utils/kdtree.h:14-18) */
+typedef struct {
+    double key[3];
+    int32_t idx;
+} dedup_slot;
+
+static uint64_t key_bits(double v)
+{
+    if (v == 0.0)
+        v = 0.0; /* -0.0 == 0.0 in the reference's comparison */
+    uint64_t b;
+    memcpy(&b, &v, 8);
+    return b;
+}
+
+static uint64_t hash3(const double *p)
+{
+    uint64_t h = key_bits(p[0]) * 0x9E3779B97F4A7C15ull;
+    h ^= key_bits(p[1]) + 0x632BE59BD9B4E019ull + (h << 6) + (h >> 2);
+    h ^= key_bits(p[2]) + 0x85EBCA77C2B2AE63ull + (h << 6) + (h >> 2);
+    return h ^ (h >> 29);
+}
+
+Pos slam_localization(SLAM_attr *attr, PointCloud *lidarPointCloud,
+                      Pos pos_predict, Pos pos_last)
+{
+    navgpu_ctx *c = ctx();
+    slam_state *s = state_for(attr);
+    double R[9];
+    rotation(pos_predict.roll, pos_predict.pitch, pos_predict.yaw, R);
+    double transform[6]; /* compute_posdiff, src/slam.c:84-92 */
+    transform[0] = pos_predict.x - pos_last.x;
+    transform[1] = pos_predict.y - pos_last.y;
+    transform[2] = pos_predict.z - pos_last.z;
+    transform[3] = pos_predict.roll - pos_last.roll;
+    transform[4] = pos_predict.pitch - pos_last.pitch;
+    transform[5] = pos_predict.yaw - pos_last.yaw;
+    double t[3] = {pos_predict.x, pos_predict.y, pos_predict.z};
+
+    /* GPU: transform, features, per-row 1-NN (src/slam.c:185-244) */
+    CK(navgpu_upload(c, s->d_lidar, &lidarPointCloud->ToF_position[0][0],
+                     24 * NPTS));
+    CK(navgpu_transform_dev(c, s->d_lidar, NPTS, R, t, transform, s->d_global,
+                            s->d_last));
+    if (!s->have_trees) { /* localisation before any init/mapping: no map */
+        CK(navgpu_upload(c, s->d_tn, (int32_t[ROWS]){0}, 4 * ROWS));
+        s->have_trees = 1;
+    }
+    CK(navgpu_kd_query_rows_dev(c, s->d_tree, s->d_tn, s->d_lidar, s->d_last,
+                                ROWS, COLS, s->d_pos, s->d_dist, NULL));
+    CK(navgpu_download(c, s->h_pos, s->d_pos, 4 * NPTS));
+    CK(navgpu_download(c, s->h_dist, s->d_dist, 8 * NPTS));
+    CK(navgpu_download(c, s->h_tp, s->d_global, 24 * NPTS));
+    CK(navgpu_sync(c));
+
+    /* host: dedup (src/slam.c:235-284) */
+    NeighborResult *result = malloc(sizeof(NeighborResult) * (NPTS ? NPTS : 1));
+    size_t tcap = 16;
+    while (tcap < 2 * (size_t)COLS)
+        tcap <<= 1;
+    dedup_slot *tab = malloc(sizeof(dedup_slot) * tcap);
+    int32_t *used = malloc(sizeof(int32_t) * tcap);
+    if (!result || !tab || !used) {
+        fprintf(stderr, "navslam: out of host memory\n");
+        abort();
+    }
+    for (size_t i = 0; i < tcap; i++)
+        tab[i].idx = -1;
+    int CPcount = 0;
+    for (int row = 0; row < ROWS; ++row) {
+        int nused = 0;
+        const double *tree = s->h_tree + 3 * (size_t)row * COLS;
+        for (int col = 0; col < COLS; ++col) {
+            size_t g = (size_t)row * COLS + col;
+            int32_t pos = s->h_pos[g];
+            /* non-feature cells, and features of an empty row tree (where the
+             * reference reads an uninitialised Point, src/slam.c:242-252):
+             * no correspondence */
+            if (pos < 0)
+                continue;
+            const double *np = tree + 3 * (size_t)pos;
+            double bestDist = s->h_dist[g];
+            int nan = np[0] != np[0] || np[1] != np[1] || np[2] != np[2];
+            size_t h = nan ? 0 : (size_t)(hash3(np) & (tcap - 1));
+            int found = -1;
+            if (!nan) {
+                while (tab[h].idx >= 0) {
+                    const double *k = tab[h].key;
+                    if (k[0] == np[0] && k[1] == np[1] && k[2] == np[2]) {
+                        found = tab[h].idx;
+                        break;
+                    }
+                    h = (h + 1) & (tcap - 1);
+                }
+            }
+            if (found >= 0) {
+                if (result[found].distance > bestDist) {
+                    memcpy(&result[found].oriPoint, s->h_tp + 3 * g, 24);
+                    memcpy(&result[found].nearestPoint, np, 24);
+                    result[found].distance = bestDist;
+                }
+                continue;
+            }
+            memcpy(&result[CPcount].oriPoint, s->h_tp + 3 * g, 24);
+            memcpy(&result[CPcount].nearestPoint, np, 24);
+            result[CPcount].distance = bestDist;
+            if (!nan) {
+                memcpy(tab[h].key, np, 24);
+                tab[h].idx = CPcount;
+                used[nused++] = (int32_t)h;
+            }
+            CPcount++;
+        }
+        for (int i = 0; i < nused; i++)
+            tab[used[i]].idx = -1;
+    }
+    free(tab);
+    free(used);
+
+    /* host: Adam on the translation (src/slam.c:218-379) */
+    double learningRate = 0.1, tolerance = 1e-6;
+    double previousTotalError = 0, totalError = 0;
+    int validGradientCount = 0;
+    double m[3] = {0.0, 0.0, 0.0}, v[3] = {0.0, 0.0, 0.0};
+    double beta1 = 0.9, beta2 = 0.999, epsilon = 1e-8;
+    int q = quiet();
+    for (int iter = 0; iter < 200; ++iter) {
+        double gradient[3] = {0.0, 0.0, 0.0};
+        totalError = 0;
+        validGradientCount = 0;
+        for (int i = 0; i < CPcount; i++) {
+            double dx = (result[i].oriPoint.x - transform[0]) - result[i].nearestPoint.x;
+            double dy = (result[i].oriPoint.y - transform[1]) - result[i].nearestPoint.y;
+            double dz = (result[i].oriPoint.z - transform[2]) - result[i].nearestPoint.z;
+            double dist_sq = dx * dx + dy * dy + dz * dz;
+            totalError += dist_sq;
+            gradient[0] -= dx;
+            gradient[1] -= dy;
+            gradient[2] -= dz;
+            validGradientCount++;
+        }
+        if (fabs(totalError - previousTotalError) < tolerance) {
+            if (!q)
+                printf("\xe6\x94\xb6\xe6\x95\x9b\xef\xbc\x8c\xe5\x81\x9c\xe6\xad\xa2"
+                       "\xe8\xbf\xad\xe4\xbb\xa3\xef\xbc\x81\n");
+            break;
+        }
+        previousTotalError = totalError;
+        if (validGradientCount > 0) {
+            gradient[0] /= validGradientCount;
+            gradient[1] /= validGradientCount;
+            gradient[2] /= validGradientCount;
+        }
+        int tt = iter + 1;
+        for (int j = 0; j < 3; j++) {
+            m[j] = beta1 * m[j] + (1 - beta1) * gradient[j];
+            v[j] = beta2 * v[j] + (1 - beta2) * gradient[j] * gradient[j];
+            double m_hat = m[j] / (1 - pow(beta1, tt));
+            double v_hat = v[j] / (1 - pow(beta2, tt));
+            transform[j] -= learningRate * m_hat / (sqrt(v_hat) + epsilon);
+        }
+        if (!q)
+            printf("Iteration %d, Total Error: %.6f\n", iter, totalError);
+    }
+    free(result);
+    if (validGradientCount > 0)
+        attr->error = sqrt(totalError / validGradientCount);
+    else
+        attr->error = 0.0;
+    Pos out;
+    out.x = pos_last.x + transform[0];
+    out.y = pos_last.y + transform[1];
+    out.z = pos_last.z + transform[2];
+    out.roll = pos_last.roll + transform[3];
+    out.pitch = pos_last.pitch + transform[4];
+    out.yaw = pos_last.yaw + transform[5];
+    return out;
+}

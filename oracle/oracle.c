@@ -308,6 +308,10 @@ void orc_knn_brute(const double *tgt, size_t nt, const double *qs, size_t nq,
             const double *tp = tgt + 3 * t;
             double dx = tp[0] - qp[0], dy = tp[1] - qp[1], dz = tp[2] - qp[2];
             double d = sqrt(dx * dx + dy * dy + dz * dz);
+            /* as the reference 1-NN (kdtree.c:117, best starts at INFINITY):
+             * an infinite or NaN distance is never a neighbour */
+            if (!(d < INFINITY))
+                continue;
             /* indices ascend, so an equal distance never displaces */
             if (have == k && !(d < bd[k - 1]))
                 continue;
@@ -586,5 +590,30 @@ void orc_ekf_update_R(orc_ekf *e, double error) /* ekf.c:114-127 */
         for (int j = 0; j < 6; j++)
             e->Rn[i][j] = 0.0;
         e->Rn[i][i] = base_R[i] * scale;
+    }
+}
+
+/* Batch drivers for the CPU baseline: the query loop stays in C so the
+ * timing measures the search, not a Python call per query. */
+void orc_kd_nn_batch(const double *tree, size_t n, const double *qs, size_t nq,
+                     long *out_pos, double *out_dist)
+{
+    for (size_t i = 0; i < nq; i++)
+        orc_kd_nn(tree, n, qs + 3 * i, out_pos + i, out_dist + i);
+}
+
+/* Calls a reference-ABI nearestNeighborSearch (utils/kdtree.c:110) through a
+ * function pointer for each query, with bestDist reset to INFINITY as
+ * src/slam.c:243 does. */
+typedef void (*orc_ref_nn_fn)(void *root, const double *target, double *result,
+                              double *bestDist, int depth);
+void orc_ref_nn_batch(void *fn, void *root, const double *qs, size_t nq,
+                      double *out_pts, double *out_dist)
+{
+    orc_ref_nn_fn f = (orc_ref_nn_fn)fn;
+    for (size_t i = 0; i < nq; i++) {
+        double best = INFINITY;
+        f(root, qs + 3 * i, out_pts + 3 * i, &best, 0);
+        out_dist[i] = best;
     }
 }

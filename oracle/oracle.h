@@ -85,10 +85,20 @@ void orc_rows_match(const double *src, const double *tgt, int R, int C,
  * utils/kdtree.c:110-152; k > 1 is a restatement): per query, the k target
  * points with the smallest reference distance (utils/kdtree.c:14-17,
  * dx = target_point - query), ordered by (distance, index) ascending, so
- * equal distances resolve to the lowest index. Missing slots (nt < k) get
- * index -1 and distance +INFINITY. Brute force, O(nq * nt). */
+ * equal distances resolve to the lowest index. Missing slots get index -1
+ * and distance +INFINITY; an infinite/NaN distance is never a neighbour
+ * (kdtree.c:117 takes a point only if dist < best, best = INFINITY).
+ * Brute force, O(nq * nt). */
 void orc_knn_brute(const double *tgt, size_t nt, const double *qs, size_t nq,
                    int k, int *out_idx, double *out_dist);
+
+/* CPU-baseline drivers: orc_kd_nn over nq queries; and a loop calling a
+ * reference-ABI nearestNeighborSearch through `fn` (bestDist = INFINITY per
+ * query, as src/slam.c:243). */
+void orc_kd_nn_batch(const double *tree, size_t n, const double *qs, size_t nq,
+                     long *out_pos, double *out_dist);
+void orc_ref_nn_batch(void *fn, void *root, const double *qs, size_t nq,
+                      double *out_pts, double *out_dist);
 
 /* ---- src/slam.c:134-431 frame loop, runtime dims, buffers sized R*C ---- */
 typedef struct orc_slam orc_slam;

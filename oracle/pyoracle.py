@@ -42,6 +42,9 @@ class Oracle:
         L.orc_kd_nn.argtypes = [_dp, C.c_size_t, _dp, C.POINTER(C.c_long), _dp]
         L.orc_rows_match.argtypes = [_dp, _dp, C.c_int, C.c_int, _ip, _ip, _ip, _dp]
         L.orc_knn_brute.argtypes = [_dp, C.c_size_t, _dp, C.c_size_t, C.c_int, _ip, _dp]
+        L.orc_kd_nn_batch.argtypes = [_dp, C.c_size_t, _dp, C.c_size_t,
+                                      C.POINTER(C.c_long), _dp]
+        L.orc_ref_nn_batch.argtypes = [C.c_void_p, C.c_void_p, _dp, C.c_size_t, _dp, _dp]
         L.orc_slam_create.restype = C.c_void_p
         L.orc_slam_create.argtypes = [C.c_int, C.c_int]
         L.orc_slam_destroy.argtypes = [C.c_void_p]
@@ -104,6 +107,22 @@ class Oracle:
         d = np.zeros(1)
         self.L.orc_kd_nn(_d(tree), len(tree), _d(q), C.byref(pos), _d(d))
         return pos.value, d[0]
+
+    def kd_nn_batch(self, tree, qs):
+        tree = np.ascontiguousarray(tree, np.float64).reshape(-1, 3)
+        qs = np.ascontiguousarray(qs, np.float64).reshape(-1, 3)
+        pos = np.zeros(len(qs), np.int64)
+        d = np.zeros(len(qs))
+        self.L.orc_kd_nn_batch(_d(tree), len(tree), _d(qs), len(qs),
+                               pos.ctypes.data_as(C.POINTER(C.c_long)), _d(d))
+        return pos, d
+
+    def ref_nn_batch(self, fn_addr, root, qs):
+        qs = np.ascontiguousarray(qs, np.float64).reshape(-1, 3)
+        pts = np.zeros_like(qs)
+        d = np.zeros(len(qs))
+        self.L.orc_ref_nn_batch(fn_addr, root, _d(qs), len(qs), _d(pts), _d(d))
+        return pts, d
 
     def rows_match(self, src, tgt):
         src = np.ascontiguousarray(src, np.float64)
