@@ -23,8 +23,10 @@
 #include <stdarg.h>
 #include <stdint.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
 #include <map>
 #include <string>
 #include <utility>
@@ -651,111 +653,120 @@ inline int kd_build_lds_bytes(int n) {
 }
 
 // ============================================================ global mode
+// Uniform grid over the target cloud. Cells are numbered x-fastest, so the
+// cells x-1..x+1 of one (y,z) row are contiguous in the cell-sorted target
+// array: a query's 3x3x3 neighbourhood is 9 contiguous "runs".
 struct GridParams {
-  double o[3];
-  double h, inv_h, delta;
+  double o[3];      // origin = target bbox min
+  double h, inv_h;  // cell edge
+  double delta;     // slack on cell boxes (cell assignment is f64 arithmetic)
+  double emax;      // largest bbox extent
   int g[3];
   int ncells;
 };
 
-struct __align__(16) Rec {  // sorted target record, 32 B
-  double x, y, z;
-  int idx, pad;
+struct __align__(16) Rec16 {  // cell-sorted target: (coords - origin) in f32
+  float x, y, z;
+  int idx;
 };
 
-constexpr int kOcc = 3;  // target points per cell
+constexpr int kBBoxBlocks = 1024;
+constexpr int kKeyBits = 8;  // local candidate id in the low bits of a key
+constexpr uint32_t kKeyMask = (1u << kKeyBits) - 1;
+constexpr uint32_t kNoKey = 0xffffffffu;
 
-__device__ __forceinline__ unsigned long long ord_enc(double v) {
-  unsigned long long u = (unsigned long long)__double_as_longlong(v);
-  return (u >> 63) ? ~u : (u | 0x8000000000000000ull);
-}
-__device__ __forceinline__ double ord_dec(unsigned long long u) {
-  u = (u >> 63) ? (u & 0x7fffffffffffffffull) : ~u;
-  return __longlong_as_double((long long)u);
-}
-
-// bbox[0..2] = ordered-min, bbox[3..5] = ordered-max (memset 0xff / 0x00)
-__global__ __launch_bounds__(256) void k_bbox(const double *__restrict__ p,
-                                              size_t n,
-                                              unsigned long long *bbox) {
-  double mn[3] = {INFINITY, INFINITY, INFINITY};
-  double mx[3] = {-INFINITY, -INFINITY, -INFINITY};
+// per-block min/max of the finite coordinates -> part[block][6]
+__global__ __launch_bounds__(256) void k_bbox_partial(const double *__restrict__ p,
+                                                      size_t n, double *__restrict__ part) {
+  __shared__ double s[4][6];
+  double v6[6] = {INFINITY, INFINITY, INFINITY, -INFINITY, -INFINITY, -INFINITY};
   for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
        i += (size_t)gridDim.x * blockDim.x) {
 #pragma unroll
     for (int a = 0; a < 3; ++a) {
       const double v = p[3 * i + a];
-      if (v == v && fabs(v) < INFINITY) {
-        mn[a] = fmin(mn[a], v);
-        mx[a] = fmax(mx[a], v);
+      if (fabs(v) < INFINITY) {
+        v6[a] = fmin(v6[a], v);
+        v6[3 + a] = fmax(v6[3 + a], v);
       }
     }
   }
 #pragma unroll
-  for (int a = 0; a < 3; ++a) {
+  for (int a = 0; a < 3; ++a)
     for (int o = kWave / 2; o > 0; o >>= 1) {
-      mn[a] = fmin(mn[a], __shfl_xor(mn[a], o, kWave));
-      mx[a] = fmax(mx[a], __shfl_xor(mx[a], o, kWave));
+      v6[a] = fmin(v6[a], __shfl_xor(v6[a], o, kWave));
+      v6[3 + a] = fmax(v6[3 + a], __shfl_xor(v6[3 + a], o, kWave));
     }
-  }
-  if ((threadIdx.x & (kWave - 1)) == 0) {
-#pragma unroll
-    for (int a = 0; a < 3; ++a) {
-      if (mn[a] <= mx[a]) {
-        atomicMin(&bbox[a], ord_enc(mn[a]));
-        atomicMax(&bbox[3 + a], ord_enc(mx[a]));
-      }
-    }
+  const int wid = threadIdx.x / kWave;
+  if ((threadIdx.x & (kWave - 1)) == 0)
+    for (int a = 0; a < 6; ++a) s[wid][a] = v6[a];
+  __syncthreads();
+  if (threadIdx.x < 6) {
+    const int a = threadIdx.x;
+    double r = s[0][a];
+    for (int w = 1; w < 4; ++w) r = a < 3 ? fmin(r, s[w][a]) : fmax(r, s[w][a]);
+    part[blockIdx.x * 6 + a] = r;
   }
 }
 
-__global__ void k_grid_params(const unsigned long long *bbox, size_t n,
-                              int cap, GridParams *gp) {
-  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+// bbox from the partials, then the grid: h for ~occ points per cell, capped
+// at `cap` cells.
+__global__ __launch_bounds__(256) void k_grid_params(const double *__restrict__ part,
+                                                     int nparts, size_t n, int cap,
+                                                     double occ, GridParams *gp) {
+  __shared__ double s[256][6];
+  double v6[6] = {INFINITY, INFINITY, INFINITY, -INFINITY, -INFINITY, -INFINITY};
+  for (int b = threadIdx.x; b < nparts; b += blockDim.x)
+    for (int a = 0; a < 6; ++a)
+      v6[a] = a < 3 ? fmin(v6[a], part[b * 6 + a]) : fmax(v6[a], part[b * 6 + a]);
+  for (int a = 0; a < 6; ++a) s[threadIdx.x][a] = v6[a];
+  __syncthreads();
+  if (threadIdx.x != 0) return;
+  for (int t = 1; t < (int)blockDim.x; ++t)
+    for (int a = 0; a < 6; ++a)
+      v6[a] = a < 3 ? fmin(v6[a], s[t][a]) : fmax(v6[a], s[t][a]);
   GridParams G;
   double lo[3], ext[3];
-  bool any = true;
+  bool any = n > 0;
   for (int a = 0; a < 3; ++a) {
-    const double l = ord_dec(bbox[a]), h = ord_dec(bbox[3 + a]);
-    if (!(l <= h)) any = false;
-    lo[a] = l;
-    ext[a] = h - l;
+    if (!(v6[a] <= v6[3 + a])) any = false;
+    lo[a] = v6[a];
+    ext[a] = v6[3 + a] - v6[a];
   }
-  if (!any || n == 0) {
+  if (!any) {
     for (int a = 0; a < 3; ++a) {
       G.o[a] = 0.0;
       G.g[a] = 1;
     }
-    G.h = 1.0;
-    G.inv_h = 1.0;
-    G.delta = 1.0;
+    G.h = G.inv_h = G.delta = 1.0;
+    G.emax = 0.0;
     G.ncells = 1;
     *gp = G;
     return;
   }
   const double emax = fmax(ext[0], fmax(ext[1], ext[2]));
-  const double floor_e = fmax(emax * 1e-6, 1e-9);
+  const double floor_e = fmax(emax * 1e-3, 1e-9);
   double vol = 1.0;
   for (int a = 0; a < 3; ++a) vol *= fmax(ext[a], floor_e);
-  double h = cbrt(vol * kOcc / (double)n);
-  if (!(h > 0)) h = 1.0;
+  double h = cbrt(vol * occ / (double)n);
+  if (!(h > 0) || !(h < INFINITY)) h = fmax(emax, 1.0);
   int g[3];
-  for (int it = 0; it < 64; ++it) {
+  for (int it = 0; it < 200; ++it) {
     long long tot = 1;
     for (int a = 0; a < 3; ++a) {
-      double ga = ceil(ext[a] / h);
-      if (ga < 1) ga = 1;
-      if (ga > 1024) ga = 1024;
+      double ga = floor(ext[a] / h) + 1.0;  // covers [lo, lo + ext] inclusive
+      if (ga > 2048) ga = 2048;
       g[a] = (int)ga;
       tot *= g[a];
     }
     if (tot <= cap) break;
-    h *= 1.26;
+    h *= 1.1;
   }
   for (int a = 0; a < 3; ++a) G.o[a] = lo[a];
   G.h = h;
   G.inv_h = 1.0 / h;
   G.delta = 1e-7 * (emax + h);
+  G.emax = emax;
   G.g[0] = g[0];
   G.g[1] = g[1];
   G.g[2] = g[2];
@@ -765,9 +776,14 @@ __global__ void k_grid_params(const unsigned long long *bbox, size_t n,
 
 __device__ __forceinline__ int cell_axis(double v, const GridParams &G, int a) {
   const double t = (v - G.o[a]) * G.inv_h;
-  if (!(t >= 0.0)) return 0;
+  if (!(t >= 0.0)) return 0;  // below the grid, or NaN
   if (t >= (double)G.g[a]) return G.g[a] - 1;
   return (int)t;
+}
+
+__device__ __forceinline__ int cell_of(const double *p, const GridParams &G) {
+  return (cell_axis(p[2], G, 2) * G.g[1] + cell_axis(p[1], G, 1)) * G.g[0] +
+         cell_axis(p[0], G, 0);
 }
 
 __global__ __launch_bounds__(256) void k_cell_count(
@@ -776,9 +792,7 @@ __global__ __launch_bounds__(256) void k_cell_count(
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const GridParams G = *gp;
-  const int cx = cell_axis(p[3 * i], G, 0), cy = cell_axis(p[3 * i + 1], G, 1),
-            cz = cell_axis(p[3 * i + 2], G, 2);
-  const int c = (cz * G.g[1] + cy) * G.g[0] + cx;
+  const int c = cell_of(p + 3 * i, G);
   cellid[i] = c;
   slot[i] = atomicAdd(&cnt[c], 1);
 }
@@ -801,7 +815,6 @@ __global__ __launch_bounds__(kScanBlock) void k_scan_sums(
 
 __global__ __launch_bounds__(kScanBlock) void k_scan_top(int *bsum, int nb) {
   __shared__ int scratch[40];
-  // nb <= kScanBlock * kScanPer
   int v[kScanPer];
   int s = 0;
 #pragma unroll
@@ -841,19 +854,27 @@ __global__ __launch_bounds__(kScanBlock) void k_scan_apply(
   }
 }
 
-__global__ __launch_bounds__(256) void k_scatter(
-    const double *__restrict__ p, size_t n, const int *__restrict__ cellid,
-    const int *__restrict__ slot, const int *__restrict__ start,
-    Rec *__restrict__ rec) {
+__global__ __launch_bounds__(256) void k_scatter_targets(
+    const double *__restrict__ p, size_t n, const GridParams *__restrict__ gp,
+    const int *__restrict__ cellid, const int *__restrict__ slot,
+    const int *__restrict__ start, Rec16 *__restrict__ rec) {
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  Rec r;
-  r.x = p[3 * i];
-  r.y = p[3 * i + 1];
-  r.z = p[3 * i + 2];
+  const GridParams G = *gp;
+  Rec16 r;
+  r.x = (float)(p[3 * i] - G.o[0]);
+  r.y = (float)(p[3 * i + 1] - G.o[1]);
+  r.z = (float)(p[3 * i + 2] - G.o[2]);
   r.idx = (int)i;
-  r.pad = 0;
   rec[start[cellid[i]] + slot[i]] = r;
+}
+
+__global__ __launch_bounds__(256) void k_scatter_queries(
+    size_t n, const int *__restrict__ cellid, const int *__restrict__ slot,
+    const int *__restrict__ start, int *__restrict__ perm) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  perm[start[cellid[i]] + slot[i]] = (int)i;
 }
 
 // (d, i) < (kd, ki): distance first, then index. Never true for d = inf/NaN.
@@ -861,27 +882,42 @@ __device__ __forceinline__ bool knn_less(double d, int i, double kd, int ki) {
   return d < kd || (d == kd && i < ki);
 }
 
+// squared distance from q to the box of cells [x0..x1] x [y0..y1] x [z0..z1]
+// grown by delta: a lower bound on the reference dsq of any point binned there
+__device__ __forceinline__ double box_d2(const GridParams &G, const double *qv,
+                                         int x0, int x1, int y0, int y1, int z0,
+                                         int z1) {
+  const int lo[3] = {x0, y0, z0}, hi[3] = {x1, y1, z1};
+  double s = 0.0;
+#pragma unroll
+  for (int a = 0; a < 3; ++a) {
+    const double bl = G.o[a] + lo[a] * G.h - G.delta;
+    const double bh = G.o[a] + (hi[a] + 1) * G.h + G.delta;
+    // boundary cells also hold everything clamped into them
+    const double e = fmax(0.0, fmax(lo[a] > 0 ? bl - qv[a] : 0.0,
+                                     hi[a] < G.g[a] - 1 ? qv[a] - bh : 0.0));
+    s += e * e;
+  }
+  return s;
+}
+
+// Exact k-NN of one query by expanding Chebyshev rings of cells: reference
+// distance in f64, (distance, index) ordering, stops when nothing outside the
+// visited block can still enter. The slow path of k_knn (rare) and the whole
+// search where the fast path's certificate cannot be given.
 template <int K>
-__global__ __launch_bounds__(256) void k_knn(
-    const GridParams *__restrict__ gp, const int *__restrict__ start,
-    const int *__restrict__ cnt, const Rec *__restrict__ rec,
-    const double *__restrict__ qs, size_t nq, int32_t *__restrict__ oidx,
-    double *__restrict__ odist) {
-  const size_t q = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (q >= nq) return;
-  const GridParams G = *gp;
-  const double qx = qs[3 * q], qy = qs[3 * q + 1], qz = qs[3 * q + 2];
-  double kd[K];
-  int ki[K];
+__device__ void knn_exact_lane(const GridParams &G, const int *__restrict__ start,
+                               const Rec16 *__restrict__ rec,
+                               const double *__restrict__ tgt, const double *qv,
+                               double *kd, int *ki) {
 #pragma unroll
   for (int s = 0; s < K; ++s) {
     kd[s] = INFINITY;
     ki[s] = -1;
   }
-  double thr = INFINITY;  // dsq admission bound for the current k-th
-  const int c[3] = {cell_axis(qx, G, 0), cell_axis(qy, G, 1),
-                    cell_axis(qz, G, 2)};
-  const double qv[3] = {qx, qy, qz};
+  double thr = INFINITY;
+  const int c[3] = {cell_axis(qv[0], G, 0), cell_axis(qv[1], G, 1),
+                    cell_axis(qv[2], G, 2)};
   const int gmax = max(G.g[0], max(G.g[1], G.g[2]));
   for (int r = 0; r <= gmax; ++r) {
     for (int dz = -r; dz <= r; ++dz) {
@@ -891,40 +927,31 @@ __global__ __launch_bounds__(256) void k_knn(
         const int y = c[1] + dy;
         if (y < 0 || y >= G.g[1]) continue;
         const bool face = (dz == -r || dz == r || dy == -r || dy == r);
-        const int step = face ? 1 : 2 * r;
-        for (int dx = -r; dx <= r; dx += (step > 0 ? step : 1)) {
+        const int step = (face || r == 0) ? 1 : 2 * r;
+        for (int dx = -r; dx <= r; dx += step) {
           const int x = c[0] + dx;
           if (x < 0 || x >= G.g[0]) continue;
-          // box lower bound (cell grown by delta)
-          const int cc[3] = {x, y, z};
-          double bd2 = 0.0;
-#pragma unroll
-          for (int a = 0; a < 3; ++a) {
-            const double lo = G.o[a] + cc[a] * G.h - G.delta;
-            const double hi = G.o[a] + (cc[a] + 1) * G.h + G.delta;
-            const double e = fmax(0.0, fmax(lo - qv[a], qv[a] - hi));
-            bd2 += e * e;
-          }
-          if (bd2 > thr) continue;
+          if (box_d2(G, qv, x, x, y, y, z, z) > thr) continue;
           const int cell = (z * G.g[1] + y) * G.g[0] + x;
-          const int b = start[cell], e = b + cnt[cell];
+          const int b = start[cell], e = start[cell + 1];
           for (int t = b; t < e; ++t) {
-            const Rec rr = rec[t];
-            const double dx2 = rr.x - qx, dy2 = rr.y - qy, dz2 = rr.z - qz;
-            const double dsq = dx2 * dx2 + dy2 * dy2 + dz2 * dz2;
+            const int id = rec[t].idx;
+            const double *tp = tgt + 3 * (size_t)id;
+            const double ddx = tp[0] - qv[0], ddy = tp[1] - qv[1], ddz = tp[2] - qv[2];
+            const double dsq = ddx * ddx + ddy * ddy + ddz * ddz;
             if (!(dsq <= thr)) continue;
             const double d = __builtin_sqrt(dsq);
-            if (!knn_less(d, rr.idx, kd[K - 1], ki[K - 1])) continue;
+            if (!knn_less(d, id, kd[K - 1], ki[K - 1])) continue;
             bool placed = false;
 #pragma unroll
             for (int s = K - 1; s >= 0; --s) {
               if (!placed) {
-                if (s > 0 && knn_less(d, rr.idx, kd[s - 1], ki[s - 1])) {
+                if (s > 0 && knn_less(d, id, kd[s - 1], ki[s - 1])) {
                   kd[s] = kd[s - 1];
                   ki[s] = ki[s - 1];
                 } else {
                   kd[s] = d;
-                  ki[s] = rr.idx;
+                  ki[s] = id;
                   placed = true;
                 }
               }
@@ -935,16 +962,164 @@ __global__ __launch_bounds__(256) void k_knn(
         }
       }
     }
-    // lower bound on any point outside the visited (2r+1)^3 block
     double L = INFINITY;
 #pragma unroll
     for (int a = 0; a < 3; ++a) {
       if (c[a] - r > 0) L = fmin(L, qv[a] - (G.o[a] + (c[a] - r) * G.h));
-      if (c[a] + r < G.g[a] - 1)
-        L = fmin(L, (G.o[a] + (c[a] + r + 1) * G.h) - qv[a]);
+      if (c[a] + r < G.g[a] - 1) L = fmin(L, (G.o[a] + (c[a] + r + 1) * G.h) - qv[a]);
     }
-    if (L == INFINITY) break;               // whole grid visited
-    if (kd[K - 1] < L - 2.0 * G.delta) break;  // k found, nothing closer left
+    if (L == INFINITY) break;
+    const double Lg = L - 2.0 * G.delta;
+    if (Lg > 0.0 && kd[K - 1] < INFINITY && thr < Lg * Lg) break;
+  }
+}
+
+__device__ __forceinline__ uint32_t umed3(uint32_t a, uint32_t b, uint32_t c) {
+  return max(min(a, b), min(max(a, b), c));
+}
+
+// Global-mode exact k-NN, one lane per (cell-sorted) query.
+// Fast path: the 9 x-runs of the 3x3x3 neighbourhood (centre run first, runs
+// whose box is already beyond the current (K+1)-th candidate skipped), an f32
+// distance per candidate packed with its local id into a 32-bit key and kept
+// in a sorted list of K+1 keys by branch-free median-of-3 insertion. Then the
+// K+1 survivors are re-evaluated with the reference f64 formula and sorted
+// by (distance, index); the result is certified exact when every candidate
+// left out (visited but not kept, skipped, or outside the block) is provably
+// farther than the K-th, using the f32 error bound. Otherwise (near ties,
+// sparse cells, overflow) the lane runs knn_exact_lane.
+template <int K>
+__global__ __launch_bounds__(256) void k_knn(
+    const GridParams *__restrict__ gp, const int *__restrict__ start,
+    const Rec16 *__restrict__ rec, const double *__restrict__ tgt,
+    const double *__restrict__ qs, const int *__restrict__ qperm, size_t nq,
+    int32_t *__restrict__ oidx, double *__restrict__ odist) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nq) return;
+  const GridParams G = *gp;
+  const size_t q = (size_t)qperm[i];
+  const double qv[3] = {qs[3 * q], qs[3 * q + 1], qs[3 * q + 2]};
+  const double qr[3] = {qv[0] - G.o[0], qv[1] - G.o[1], qv[2] - G.o[2]};
+  const float qf[3] = {(float)qr[0], (float)qr[1], (float)qr[2]};
+  const int c[3] = {cell_axis(qv[0], G, 0), cell_axis(qv[1], G, 1),
+                    cell_axis(qv[2], G, 2)};
+  // |f32 coordinate difference - exact difference| <= dl (MI-free bound:
+  // both operands rounded to f32 once, then one f32 subtraction)
+  const double Dq = fmax(G.emax + G.h,
+                         fmax(fabs(qr[0]), fmax(fabs(qr[1]), fabs(qr[2]))));
+  const double dl = Dq * 0x1p-21;
+  constexpr int KL = K + 1;
+  uint32_t key[KL];
+#pragma unroll
+  for (int s = 0; s < KL; ++s) key[s] = kNoKey;
+  int rb[9], rl[9];
+  int lid = 0;
+  const int x0 = max(c[0] - 1, 0), x1 = min(c[0] + 1, G.g[0] - 1);
+#pragma unroll
+  for (int r = 0; r < 9; ++r) {
+    const int dyv = r == 0 ? 0 : (r == 1 ? -1 : (r == 2 ? 1 : (r <= 4 ? 0 : (r & 1 ? -1 : 1))));
+    const int dzv = r <= 2 ? 0 : (r == 3 ? -1 : (r == 4 ? 1 : (r <= 6 ? -1 : 1)));
+    rb[r] = 0;
+    rl[r] = lid;
+    const int y = c[1] + dyv, z = c[2] + dzv;
+    if (y < 0 || y >= G.g[1] || z < 0 || z >= G.g[2]) continue;
+    if (r > 0 && key[K] != kNoKey) {
+      const double V = (double)__uint_as_float(key[K] & ~kKeyMask);
+      if (box_d2(G, qv, x0, x1, y, y, z, z) > V) continue;
+    }
+    const int cb = (z * G.g[1] + y) * G.g[0];
+    const int t0 = start[cb + x0], t1 = start[cb + x1 + 1];
+    rb[r] = t0;
+    for (int t = t0; t < t1; t += 4) {
+      // four loads in flight before the first is consumed
+      Rec16 rr[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) rr[j] = rec[t + j < t1 ? t + j : t0];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float dx = rr[j].x - qf[0], dy = rr[j].y - qf[1], dz = rr[j].z - qf[2];
+        const float d2 = __builtin_fmaf(dz, dz, __builtin_fmaf(dy, dy, dx * dx));
+        uint32_t kk = (__float_as_uint(d2) & ~kKeyMask) | (uint32_t)((lid + j) & kKeyMask);
+        // inf / NaN: never a neighbour; past the run end: padding
+        if (!(d2 <= 3.0e38f) || t + j >= t1) kk = kNoKey;
+#pragma unroll
+        for (int s = K; s > 0; --s) key[s] = umed3(key[s - 1], key[s], kk);
+        key[0] = min(key[0], kk);
+      }
+      lid += min(4, t1 - t);
+    }
+  }
+  // anything outside the 3x3x3 block is at least L away
+  double L = INFINITY;
+#pragma unroll
+  for (int a = 0; a < 3; ++a) {
+    if (c[a] - 1 > 0) L = fmin(L, qv[a] - (G.o[a] + (c[a] - 1) * G.h));
+    if (c[a] + 1 < G.g[a] - 1) L = fmin(L, (G.o[a] + (c[a] + 2) * G.h) - qv[a]);
+  }
+  double B = INFINITY;  // lower bound on the exact dsq of every excluded point
+  if (L < INFINITY) {
+    const double Lg = L - 2.0 * G.delta;
+    B = Lg > 0.0 ? Lg * Lg : 0.0;
+  }
+  if (key[K] != kNoKey) {
+    const double V = (double)__uint_as_float(key[K] & ~kKeyMask);
+    const double err = V * 0x1p-20 + 4.0 * dl * __builtin_sqrt(V) + 4.0 * dl * dl;
+    B = fmin(B, V - err);
+  }
+  bool ok = lid <= (int)(kKeyMask + 1) && Dq < 1e17;
+  double ed[KL], e2[KL];
+  int ei[KL];
+#pragma unroll
+  for (int s = 0; s < KL; ++s) {
+    ed[s] = INFINITY;
+    e2[s] = INFINITY;
+    ei[s] = -1;
+    if (key[s] != kNoKey) {
+      const int l = (int)(key[s] & kKeyMask);
+      int t = 0;
+#pragma unroll
+      for (int r = 0; r < 9; ++r)
+        if (rl[r] <= l) t = rb[r] + (l - rl[r]);
+      const int id = rec[t].idx;
+      const double *tp = tgt + 3 * (size_t)id;
+      const double ddx = tp[0] - qv[0], ddy = tp[1] - qv[1], ddz = tp[2] - qv[2];
+      const double dsq = ddx * ddx + ddy * ddy + ddz * ddz;  // utils/kdtree.c:16
+      e2[s] = dsq;
+      ed[s] = __builtin_sqrt(dsq);
+      ei[s] = id;
+    }
+  }
+  // insertion sort by (distance, index); f32 order is almost always right
+#pragma unroll
+  for (int s = 1; s < KL; ++s) {
+#pragma unroll
+    for (int u = s; u > 0; --u) {
+      const bool sw = knn_less(ed[u], ei[u], ed[u - 1], ei[u - 1]);
+      const double td = ed[u], t2 = e2[u];
+      const int ti = ei[u];
+      ed[u] = sw ? ed[u - 1] : ed[u];
+      e2[u] = sw ? e2[u - 1] : e2[u];
+      ei[u] = sw ? ei[u - 1] : ei[u];
+      ed[u - 1] = sw ? td : ed[u - 1];
+      e2[u - 1] = sw ? t2 : e2[u - 1];
+      ei[u - 1] = sw ? ti : ei[u - 1];
+    }
+  }
+  const double dk2 = e2[K - 1];
+  if (dk2 < INFINITY)
+    ok = ok && B > dk2 * (1.0 + 0x1p-48);
+  else
+    ok = ok && B == INFINITY;  // fewer than K neighbours: only if all was seen
+  double kd[K];
+  int ki[K];
+  if (ok) {
+#pragma unroll
+    for (int s = 0; s < K; ++s) {
+      kd[s] = ed[s];
+      ki[s] = ei[s];
+    }
+  } else {
+    knn_exact_lane<K>(G, start, rec, tgt, qv, kd, ki);
   }
 #pragma unroll
   for (int s = 0; s < K; ++s) {
@@ -966,13 +1141,14 @@ struct navgpu_ctx {
   std::vector<hipEvent_t> free_ev;
   std::vector<double> tan_c, tan_r;
   int tan_R = -1, tan_C = -1;
+  double knn_occ = 3.0;  // target points per grid cell (NAVGPU_KNN_OCC)
 };
 
 namespace {
 
 enum Slot {
   kBBox = 1, kParams, kCnt, kStart, kBSum, kCellId, kSlotBuf, kRec, kTan,
-  kKdFc, kKdP, kKdT,
+  kKdFc, kKdP, kKdT, kQStart, kQCell, kQSlot, kQPerm,
   kH0 = 100, kH1, kH2, kH3, kH4, kH5,
 };
 
@@ -1103,6 +1279,10 @@ int navgpu_create(int device, void *stream, navgpu_ctx **out) {
   HIP_TRY(hipSetDevice(device));
   navgpu_ctx *c = new navgpu_ctx();
   c->device = device;
+  if (const char *o = getenv("NAVGPU_KNN_OCC")) {
+    const double v = atof(o);
+    if (v > 0.05 && v < 1000) c->knn_occ = v;
+  }
   if (stream) {
     c->stream = (hipStream_t)stream;
   } else {
@@ -1477,63 +1657,85 @@ int navgpu_knn_dev(navgpu_ctx *ctx, const double *tgt, size_t nt,
                    const double *queries, size_t nq, int k, int32_t *idx,
                    double *dist) {
   ARG_CHECK(ctx && k >= 1 && k <= 16);
-  ARG_CHECK(nt < (size_t)INT32_MAX && nq < ((size_t)1 << 40));
+  ARG_CHECK(nt < (size_t)INT32_MAX / 2 && nq < (size_t)INT32_MAX);
   if (!nq) return NAVGPU_OK;
   ARG_CHECK(queries && idx && dist && (tgt || nt == 0));
-  const int cap = (int)(nt / kOcc) * 2 + 1024;
-  unsigned long long *bbox;
-  GridParams *gp;
-  int *cnt, *start, *bsum, *cellid = nullptr, *slot = nullptr;
-  Rec *rec = nullptr;
-  RC(ws(ctx, kBBox, 6, &bbox));
-  RC(ws(ctx, kParams, 1, &gp));
-  RC(ws(ctx, kCnt, cap, &cnt));
-  RC(ws(ctx, kStart, cap, &start));
-  const int nb = (cap + kScanTile - 1) / kScanTile;
+  const double occ = ctx->knn_occ;
+  const long long capl = (long long)((double)nt / occ) * 2 + 1024;
+  ARG_CHECK(capl < INT32_MAX / 2);
+  const int cap = (int)capl;
+  const int nscan = cap + 1;  // start[] has one entry past the last cell
+  const int nb = (nscan + kScanTile - 1) / kScanTile;
   if (nb > kScanTile) {
     set_err("knn: %zu targets exceed the scan capacity", nt);
     return NAVGPU_ERANGE;
   }
+  const int nparts = (int)std::min<size_t>(kBBoxBlocks, std::max<size_t>(1, grid1d(nt, 256)));
+  double *part;
+  GridParams *gp;
+  int *tcnt, *tstart, *qcnt, *qstart, *bsum, *tcell = nullptr, *tslot = nullptr;
+  int *qcell, *qslot, *qperm;
+  Rec16 *rec = nullptr;
+  RC(ws(ctx, kBBox, (size_t)kBBoxBlocks * 6, &part));
+  RC(ws(ctx, kParams, 1, &gp));
+  RC(ws(ctx, kCnt, 2 * (size_t)nscan, &tcnt));
+  qcnt = tcnt + nscan;
+  RC(ws(ctx, kStart, nscan, &tstart));
+  RC(ws(ctx, kQStart, nscan, &qstart));
   RC(ws(ctx, kBSum, nb, &bsum));
   if (nt) {
-    RC(ws(ctx, kCellId, nt, &cellid));
-    RC(ws(ctx, kSlotBuf, nt, &slot));
+    RC(ws(ctx, kCellId, nt, &tcell));
+    RC(ws(ctx, kSlotBuf, nt, &tslot));
     RC(ws(ctx, kRec, nt, &rec));
   }
+  RC(ws(ctx, kQCell, nq, &qcell));
+  RC(ws(ctx, kQSlot, nq, &qslot));
+  RC(ws(ctx, kQPerm, nq, &qperm));
   hipStream_t s = ctx->stream;
-  HIP_TRY(hipMemsetAsync(bbox, 0xff, 24, s));
-  HIP_TRY(hipMemsetAsync(bbox + 3, 0x00, 24, s));
-  HIP_TRY(hipMemsetAsync(cnt, 0, 4 * (size_t)cap, s));
-  if (nt) {
-    const unsigned gb = (unsigned)std::min<size_t>(grid1d(nt, 256), 2048);
-    hipLaunchKernelGGL(k_bbox, dim3(gb), dim3(256), 0, s, tgt, nt, bbox);
-    CHECK_LAUNCH("k_bbox");
-  }
-  hipLaunchKernelGGL(k_grid_params, dim3(1), dim3(64), 0, s, bbox, nt, cap, gp);
-  CHECK_LAUNCH("k_grid_params");
-  if (nt) {
-    hipLaunchKernelGGL(k_cell_count, dim3(grid1d(nt, 256)), dim3(256), 0, s,
-                       tgt, nt, gp, cnt, cellid, slot);
-    CHECK_LAUNCH("k_cell_count");
-  }
-  hipLaunchKernelGGL(k_scan_sums, dim3(nb), dim3(kScanBlock), 0, s, cnt, cap, bsum);
-  CHECK_LAUNCH("k_scan_sums");
-  hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(kScanBlock), 0, s, bsum, nb);
-  CHECK_LAUNCH("k_scan_top");
-  hipLaunchKernelGGL(k_scan_apply, dim3(nb), dim3(kScanBlock), 0, s, cnt, cap,
-                     bsum, start);
-  CHECK_LAUNCH("k_scan_apply");
-  if (nt) {
-    hipLaunchKernelGGL(k_scatter, dim3(grid1d(nt, 256)), dim3(256), 0, s, tgt,
-                       nt, cellid, slot, start, rec);
-    CHECK_LAUNCH("k_scatter");
+  HIP_TRY(hipMemsetAsync(tcnt, 0, 2 * 4 * (size_t)nscan, s));
+  {
+    TimedRegion tb(ctx, "knn_build");
+    if (nt) {
+      hipLaunchKernelGGL(k_bbox_partial, dim3(nparts), dim3(256), 0, s, tgt, nt, part);
+      CHECK_LAUNCH("k_bbox_partial");
+    }
+    hipLaunchKernelGGL(k_grid_params, dim3(1), dim3(256), 0, s, part, nt ? nparts : 0,
+                       nt, cap, occ, gp);
+    CHECK_LAUNCH("k_grid_params");
+    if (nt) {
+      hipLaunchKernelGGL(k_cell_count, dim3(grid1d(nt, 256)), dim3(256), 0, s, tgt, nt,
+                         gp, tcnt, tcell, tslot);
+      CHECK_LAUNCH("k_cell_count");
+    }
+    hipLaunchKernelGGL(k_cell_count, dim3(grid1d(nq, 256)), dim3(256), 0, s, queries,
+                       nq, gp, qcnt, qcell, qslot);
+    CHECK_LAUNCH("k_cell_count(q)");
+    for (int pass = 0; pass < 2; ++pass) {
+      const int *in = pass ? qcnt : tcnt;
+      int *out = pass ? qstart : tstart;
+      hipLaunchKernelGGL(k_scan_sums, dim3(nb), dim3(kScanBlock), 0, s, in, nscan, bsum);
+      CHECK_LAUNCH("k_scan_sums");
+      hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(kScanBlock), 0, s, bsum, nb);
+      CHECK_LAUNCH("k_scan_top");
+      hipLaunchKernelGGL(k_scan_apply, dim3(nb), dim3(kScanBlock), 0, s, in, nscan,
+                         bsum, out);
+      CHECK_LAUNCH("k_scan_apply");
+    }
+    if (nt) {
+      hipLaunchKernelGGL(k_scatter_targets, dim3(grid1d(nt, 256)), dim3(256), 0, s, tgt,
+                         nt, gp, tcell, tslot, tstart, rec);
+      CHECK_LAUNCH("k_scatter_targets");
+    }
+    hipLaunchKernelGGL(k_scatter_queries, dim3(grid1d(nq, 256)), dim3(256), 0, s, nq,
+                       qcell, qslot, qstart, qperm);
+    CHECK_LAUNCH("k_scatter_queries");
   }
   TimedRegion tr(ctx, "knn_query");
   const dim3 g(grid1d(nq, 256)), b(256);
-#define KNN_CASE(KK)                                                         \
-  case KK:                                                                   \
-    hipLaunchKernelGGL(k_knn<KK>, g, b, 0, s, gp, start, cnt, rec, queries, \
-                       nq, idx, dist);                                       \
+#define KNN_CASE(KK)                                                            \
+  case KK:                                                                      \
+    hipLaunchKernelGGL(k_knn<KK>, g, b, 0, s, gp, tstart, rec, tgt, queries,   \
+                       qperm, nq, idx, dist);                                   \
     break;
   switch (k) {
     KNN_CASE(1)
