@@ -172,6 +172,10 @@ int navgpu_download(navgpu_ctx *ctx, void *dst_host, const void *src_dev,
 void navgpu_timing_enable(navgpu_ctx *ctx, int on);
 double navgpu_timing_read(navgpu_ctx *ctx, const char *name, int reset);
 int navgpu_timing_count(navgpu_ctx *ctx, const char *name);
+/* Diagnostic: queries of the last navgpu_knn_* call that left the fast path
+ * for the exact ring search (synchronises). Recorded only when the context
+ * was created with NAVGPU_KNN_STATS=1 in the environment; -1 otherwise. */
+long long navgpu_knn_fallbacks(navgpu_ctx *ctx);
 
 #ifdef __cplusplus
 }

@@ -993,7 +993,8 @@ __global__ __launch_bounds__(256) void k_knn(
     const GridParams *__restrict__ gp, const int *__restrict__ start,
     const Rec16 *__restrict__ rec, const double *__restrict__ tgt,
     const double *__restrict__ qs, const int *__restrict__ qperm, size_t nq,
-    int32_t *__restrict__ oidx, double *__restrict__ odist) {
+    int32_t *__restrict__ oidx, double *__restrict__ odist,
+    unsigned long long *__restrict__ nslow) {
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= nq) return;
   const GridParams G = *gp;
@@ -1119,6 +1120,7 @@ __global__ __launch_bounds__(256) void k_knn(
       ki[s] = ei[s];
     }
   } else {
+    if (nslow) atomicAdd(nslow, 1ull);
     knn_exact_lane<K>(G, start, rec, tgt, qv, kd, ki);
   }
 #pragma unroll
@@ -1142,13 +1144,14 @@ struct navgpu_ctx {
   std::vector<double> tan_c, tan_r;
   int tan_R = -1, tan_C = -1;
   double knn_occ = 3.0;  // target points per grid cell (NAVGPU_KNN_OCC)
+  bool knn_stats = false;
 };
 
 namespace {
 
 enum Slot {
   kBBox = 1, kParams, kCnt, kStart, kBSum, kCellId, kSlotBuf, kRec, kTan,
-  kKdFc, kKdP, kKdT, kQStart, kQCell, kQSlot, kQPerm,
+  kKdFc, kKdP, kKdT, kQStart, kQCell, kQSlot, kQPerm, kStats,
   kH0 = 100, kH1, kH2, kH3, kH4, kH5,
 };
 
@@ -1279,6 +1282,7 @@ int navgpu_create(int device, void *stream, navgpu_ctx **out) {
   HIP_TRY(hipSetDevice(device));
   navgpu_ctx *c = new navgpu_ctx();
   c->device = device;
+  if (const char *st = getenv("NAVGPU_KNN_STATS")) c->knn_stats = *st && *st != '0';
   if (const char *o = getenv("NAVGPU_KNN_OCC")) {
     const double v = atof(o);
     if (v > 0.05 && v < 1000) c->knn_occ = v;
@@ -1369,6 +1373,15 @@ double navgpu_timing_read(navgpu_ctx *ctx, const char *name, int reset) {
     it->second.clear();
   }
   return ms;
+}
+
+long long navgpu_knn_fallbacks(navgpu_ctx *ctx) {
+  if (!ctx || !ctx->knn_stats) return -1;
+  auto it = ctx->bufs.find(kStats);
+  if (it == ctx->bufs.end() || !it->second.first) return -1;
+  unsigned long long v = 0;
+  if (hipMemcpy(&v, it->second.first, 8, hipMemcpyDeviceToHost) != hipSuccess) return -1;
+  return (long long)v;
 }
 
 int navgpu_timing_count(navgpu_ctx *ctx, const char *name) {
@@ -1730,12 +1743,17 @@ int navgpu_knn_dev(navgpu_ctx *ctx, const double *tgt, size_t nt,
                        qcell, qslot, qstart, qperm);
     CHECK_LAUNCH("k_scatter_queries");
   }
+  unsigned long long *nslow = nullptr;
+  if (ctx->knn_stats) {
+    RC(ws(ctx, kStats, 1, &nslow));
+    HIP_TRY(hipMemsetAsync(nslow, 0, 8, s));
+  }
   TimedRegion tr(ctx, "knn_query");
   const dim3 g(grid1d(nq, 256)), b(256);
 #define KNN_CASE(KK)                                                            \
   case KK:                                                                      \
     hipLaunchKernelGGL(k_knn<KK>, g, b, 0, s, gp, tstart, rec, tgt, queries,   \
-                       qperm, nq, idx, dist);                                   \
+                       qperm, nq, idx, dist, nslow);                            \
     break;
   switch (k) {
     KNN_CASE(1)

@@ -61,6 +61,7 @@ def _declare(L):
         "navgpu_timing_enable": (None, [_vp, C.c_int]),
         "navgpu_timing_read": (C.c_double, [_vp, C.c_char_p, C.c_int]),
         "navgpu_timing_count": (C.c_int, [_vp, C.c_char_p]),
+        "navgpu_knn_fallbacks": (C.c_longlong, [_vp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -76,6 +77,13 @@ def load_library(path=LIBNAVGPU):
     """Load libnavgpu.so (raises if it was not built)."""
     global _LIB
     if _LIB is None:
+        # Bind to the HIP runtime torch ships when torch is present: torch loads
+        # its bundled libamdhip64 (SONAME libamdhip64.so.7) by path, so loading
+        # /opt/rocm's copy first would leave two HSA runtimes in the process.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         if not os.path.exists(path):
             raise NavGpuError(
                 f"{path} is missing: build it with `make -C nav-slam_amd` "
@@ -139,6 +147,11 @@ class NavGpu:
 
     def timing(self, on=True):
         self.L.navgpu_timing_enable(self.h, 1 if on else 0)
+
+    def knn_fallbacks(self):
+        """Queries of the last knn call that took the exact slow path (-1 if
+        not recorded; set NAVGPU_KNN_STATS=1 before creating the context)."""
+        return self.L.navgpu_knn_fallbacks(self.h)
 
     def timing_read(self, name, reset=True):
         n = self.L.navgpu_timing_count(self.h, name.encode())

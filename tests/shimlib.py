@@ -56,6 +56,8 @@ class Shim:
     def __init__(self, R, Cc):
         self.R, self.C = R, Cc
         self.path = os.path.join(LIBDIR, f"libnavslam_{R}x{Cc}.so")
+        from navslam.gpu import load_library
+        load_library()  # libnavgpu bound to the process's (torch's) HIP runtime
         L = self.L = C.CDLL(self.path)
         self.PointCloud, self.SLAMAttr = make_types(R, Cc)
         PC, SA = self.PointCloud, self.SLAMAttr
