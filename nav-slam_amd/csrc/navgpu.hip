@@ -901,21 +901,35 @@ __device__ __forceinline__ double box_d2(const GridParams &G, const double *qv,
   return s;
 }
 
+// f32 admission bound for an f64 dsq bound T: every candidate whose exact
+// dsq is <= T has an f32 dsq (coordinates relative to the grid origin, each
+// f32 difference within dl of the exact one) <= the returned value.
+__device__ __forceinline__ float f32_bound(double T, double dl) {
+  if (!(T < INFINITY)) return INFINITY;
+  const double E = T * 0x1p-20 + 4.0 * dl * __builtin_sqrt(T) + 4.0 * dl * dl;
+  return (float)((T + E) * (1.0 + 0x1p-20));
+}
+
 // Exact k-NN of one query by expanding Chebyshev rings of cells: reference
 // distance in f64, (distance, index) ordering, stops when nothing outside the
-// visited block can still enter. The slow path of k_knn (rare) and the whole
-// search where the fast path's certificate cannot be given.
+// visited block can still enter. thr0 is an upper bound on the K-th best dsq
+// (x (1 + 2^-48)) known beforehand (INFINITY if none); an f32 distance on the
+// cell-sorted records screens every candidate before its f64 coordinates are
+// loaded. The slow path of k_knn: near ties the fast path cannot certify,
+// and queries whose neighbourhood reaches past the 3x3x3 block.
 template <int K>
 __device__ void knn_exact_lane(const GridParams &G, const int *__restrict__ start,
                                const Rec16 *__restrict__ rec,
                                const double *__restrict__ tgt, const double *qv,
+                               const float *qf, double dl, double thr0,
                                double *kd, int *ki) {
 #pragma unroll
   for (int s = 0; s < K; ++s) {
     kd[s] = INFINITY;
     ki[s] = -1;
   }
-  double thr = INFINITY;
+  double thr = thr0;
+  float thr_f = f32_bound(thr, dl);
   const int c[3] = {cell_axis(qv[0], G, 0), cell_axis(qv[1], G, 1),
                     cell_axis(qv[2], G, 2)};
   const int gmax = max(G.g[0], max(G.g[1], G.g[2]));
@@ -935,7 +949,11 @@ __device__ void knn_exact_lane(const GridParams &G, const int *__restrict__ star
           const int cell = (z * G.g[1] + y) * G.g[0] + x;
           const int b = start[cell], e = start[cell + 1];
           for (int t = b; t < e; ++t) {
-            const int id = rec[t].idx;
+            const Rec16 rr = rec[t];
+            const float fx = rr.x - qf[0], fy = rr.y - qf[1], fz = rr.z - qf[2];
+            const float d2f = __builtin_fmaf(fz, fz, __builtin_fmaf(fy, fy, fx * fx));
+            if (!(d2f <= thr_f)) continue;
+            const int id = rr.idx;
             const double *tp = tgt + 3 * (size_t)id;
             const double ddx = tp[0] - qv[0], ddy = tp[1] - qv[1], ddz = tp[2] - qv[2];
             const double dsq = ddx * ddx + ddy * ddy + ddz * ddz;
@@ -957,7 +975,10 @@ __device__ void knn_exact_lane(const GridParams &G, const int *__restrict__ star
               }
             }
             const double w = kd[K - 1];
-            thr = w < INFINITY ? w * w * (1.0 + 0x1p-48) : INFINITY;
+            if (w < INFINITY) {
+              thr = fmin(thr, w * w * (1.0 + 0x1p-48));
+              thr_f = f32_bound(thr, dl);
+            }
           }
         }
       }
@@ -970,7 +991,8 @@ __device__ void knn_exact_lane(const GridParams &G, const int *__restrict__ star
     }
     if (L == INFINITY) break;
     const double Lg = L - 2.0 * G.delta;
-    if (Lg > 0.0 && kd[K - 1] < INFINITY && thr < Lg * Lg) break;
+    // every point with dsq <= thr lies inside the visited block
+    if (Lg > 0.0 && thr < Lg * Lg) break;
   }
 }
 
@@ -1121,7 +1143,9 @@ __global__ __launch_bounds__(256) void k_knn(
     }
   } else {
     if (nslow) atomicAdd(nslow, 1ull);
-    knn_exact_lane<K>(G, start, rec, tgt, qv, kd, ki);
+    // K listed points have dsq <= dk2: a valid starting bound
+    const double thr0 = dk2 < INFINITY ? dk2 * (1.0 + 0x1p-48) : INFINITY;
+    knn_exact_lane<K>(G, start, rec, tgt, qv, qf, dl, thr0, kd, ki);
   }
 #pragma unroll
   for (int s = 0; s < K; ++s) {
