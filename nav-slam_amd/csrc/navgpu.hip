@@ -663,6 +663,7 @@ struct GridParams {
   double emax;      // largest bbox extent
   int g[3];
   int ncells;
+  int tile_w;       // cells per k_knn tile along x
 };
 
 struct __align__(16) Rec16 {  // cell-sorted target: (coords - origin) in f32
@@ -671,7 +672,8 @@ struct __align__(16) Rec16 {  // cell-sorted target: (coords - origin) in f32
 };
 
 constexpr int kBBoxBlocks = 1024;
-constexpr int kKeyBits = 8;  // local candidate id in the low bits of a key
+constexpr int kKeyBits = 11;  // local id in the low bits of a key: run (4) | offset (7)
+constexpr int kRunOffBits = 7;
 constexpr uint32_t kKeyMask = (1u << kKeyBits) - 1;
 constexpr uint32_t kNoKey = 0xffffffffu;
 
@@ -713,7 +715,8 @@ __global__ __launch_bounds__(256) void k_bbox_partial(const double *__restrict__
 // at `cap` cells.
 __global__ __launch_bounds__(256) void k_grid_params(const double *__restrict__ part,
                                                      int nparts, size_t n, int cap,
-                                                     double occ, GridParams *gp) {
+                                                     double occ, size_t nq,
+                                                     GridParams *gp) {
   __shared__ double s[256][6];
   double v6[6] = {INFINITY, INFINITY, INFINITY, -INFINITY, -INFINITY, -INFINITY};
   for (int b = threadIdx.x; b < nparts; b += blockDim.x)
@@ -741,6 +744,7 @@ __global__ __launch_bounds__(256) void k_grid_params(const double *__restrict__ 
     G.h = G.inv_h = G.delta = 1.0;
     G.emax = 0.0;
     G.ncells = 1;
+    G.tile_w = 1;
     *gp = G;
     return;
   }
@@ -771,6 +775,11 @@ __global__ __launch_bounds__(256) void k_grid_params(const double *__restrict__ 
   G.g[1] = g[1];
   G.g[2] = g[2];
   G.ncells = g[0] * g[1] * g[2];
+  // tile width: ~220 queries per 256-thread tile, and its 9 staged row
+  // segments of W+2 cells within ~90 % of the LDS record budget
+  const double occ_q = (double)nq / G.ncells, occ_t = (double)n / G.ncells;
+  double w = fmin(220.0 / fmax(occ_q, 1e-9), 0.9 * 2048 / (9.0 * fmax(occ_t, 1e-9)) - 2.0);
+  G.tile_w = (int)fmax(1.0, fmin(64.0, floor(w)));
   *gp = G;
 }
 
@@ -1000,34 +1009,39 @@ __device__ __forceinline__ uint32_t umed3(uint32_t a, uint32_t b, uint32_t c) {
   return max(min(a, b), min(max(a, b), c));
 }
 
-// Global-mode exact k-NN, one lane per (cell-sorted) query.
-// Fast path: the 9 x-runs of the 3x3x3 neighbourhood (centre run first, runs
-// whose box is already beyond the current (K+1)-th candidate skipped), an f32
-// distance per candidate packed with its local id into a 32-bit key and kept
-// in a sorted list of K+1 keys by branch-free median-of-3 insertion. Then the
-// K+1 survivors are re-evaluated with the reference f64 formula and sorted
-// by (distance, index); the result is certified exact when every candidate
-// left out (visited but not kept, skipped, or outside the block) is provably
-// farther than the K-th, using the f32 error bound. Otherwise (near ties,
-// sparse cells, overflow) the lane runs knn_exact_lane.
-template <int K>
-__global__ __launch_bounds__(256) void k_knn(
-    const GridParams *__restrict__ gp, const int *__restrict__ start,
-    const Rec16 *__restrict__ rec, const double *__restrict__ tgt,
-    const double *__restrict__ qs, const int *__restrict__ qperm, size_t nq,
-    int32_t *__restrict__ oidx, double *__restrict__ odist,
-    unsigned long long *__restrict__ nslow) {
-  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= nq) return;
-  const GridParams G = *gp;
-  const size_t q = (size_t)qperm[i];
-  const double qv[3] = {qs[3 * q], qs[3 * q + 1], qs[3 * q + 2]};
+// (dy, dz) of the 9 runs of a 3x3x3 neighbourhood: centre, faces, corners
+__device__ __forceinline__ void run_dydz(int r, int &dy, int &dz) {
+  dy = r == 0 ? 0 : (r == 1 ? -1 : (r == 2 ? 1 : (r <= 4 ? 0 : (r & 1 ? -1 : 1))));
+  dz = r <= 2 ? 0 : (r == 3 ? -1 : (r == 4 ? 1 : (r <= 6 ? -1 : 1)));
+}
+
+// One query of the global-mode k-NN.
+// Fast path: the 9 x-runs of the query's 3x3x3 neighbourhood, [rb[r], re[r])
+// in the index space of `fetch` (LDS tile or global array), centre run first;
+// a run whose cell box is already beyond the current (K+1)-th candidate is
+// skipped. Each candidate gets an f32 distance packed with its local id into a
+// 32-bit key; a sorted list of K+1 keys is kept by branch-free median-of-3
+// insertion. The K+1 survivors are then re-evaluated with the reference f64
+// formula and sorted by (distance, index); the result is certified exact when
+// every candidate left out (visited but not kept, skipped, or outside the
+// block) is provably farther than the K-th, using the f32 error bound.
+// Otherwise (near ties, sparse cells, lid overflow) the lane runs
+// knn_exact_lane over the global arrays.
+struct KnnLists {
+  int *ovf_tiles, *n_ovf;  // tiles whose segments overflow the LDS budget
+  int *slow_q, *n_slow;    // queries the fast path could not certify
+  double *slow_thr;        // their starting bound (K-th dsq upper bound)
+};
+
+template <int K, class Runs, class Fetch>
+__device__ __forceinline__ void knn_one(
+    const GridParams &G, const double *__restrict__ tgt, const double qv[3],
+    const int c[3], size_t q, Runs runs, Fetch fetch,
+    int32_t *__restrict__ oidx, double *__restrict__ odist, const KnnLists &L_) {
   const double qr[3] = {qv[0] - G.o[0], qv[1] - G.o[1], qv[2] - G.o[2]};
   const float qf[3] = {(float)qr[0], (float)qr[1], (float)qr[2]};
-  const int c[3] = {cell_axis(qv[0], G, 0), cell_axis(qv[1], G, 1),
-                    cell_axis(qv[2], G, 2)};
-  // |f32 coordinate difference - exact difference| <= dl (MI-free bound:
-  // both operands rounded to f32 once, then one f32 subtraction)
+  // |f32 coordinate difference - exact difference| <= dl: both operands
+  // rounded to f32 once (relative 2^-24), then one f32 subtraction
   const double Dq = fmax(G.emax + G.h,
                          fmax(fabs(qr[0]), fmax(fabs(qr[1]), fabs(qr[2]))));
   const double dl = Dq * 0x1p-21;
@@ -1035,41 +1049,38 @@ __global__ __launch_bounds__(256) void k_knn(
   uint32_t key[KL];
 #pragma unroll
   for (int s = 0; s < KL; ++s) key[s] = kNoKey;
-  int rb[9], rl[9];
-  int lid = 0;
+  bool overflow = false;  // a run longer than 2^kRunOffBits candidates
   const int x0 = max(c[0] - 1, 0), x1 = min(c[0] + 1, G.g[0] - 1);
-#pragma unroll
+#pragma unroll 1
   for (int r = 0; r < 9; ++r) {
-    const int dyv = r == 0 ? 0 : (r == 1 ? -1 : (r == 2 ? 1 : (r <= 4 ? 0 : (r & 1 ? -1 : 1))));
-    const int dzv = r <= 2 ? 0 : (r == 3 ? -1 : (r == 4 ? 1 : (r <= 6 ? -1 : 1)));
-    rb[r] = 0;
-    rl[r] = lid;
-    const int y = c[1] + dyv, z = c[2] + dzv;
-    if (y < 0 || y >= G.g[1] || z < 0 || z >= G.g[2]) continue;
+    int t0, t1;
+    runs(r, t0, t1);
+    if (t0 >= t1) continue;
     if (r > 0 && key[K] != kNoKey) {
+      int dyv, dzv;
+      run_dydz(r, dyv, dzv);
       const double V = (double)__uint_as_float(key[K] & ~kKeyMask);
-      if (box_d2(G, qv, x0, x1, y, y, z, z) > V) continue;
+      if (box_d2(G, qv, x0, x1, c[1] + dyv, c[1] + dyv, c[2] + dzv, c[2] + dzv) > V)
+        continue;
     }
-    const int cb = (z * G.g[1] + y) * G.g[0];
-    const int t0 = start[cb + x0], t1 = start[cb + x1 + 1];
-    rb[r] = t0;
+    overflow |= (t1 - t0) > (1 << kRunOffBits);
+    const uint32_t rid = (uint32_t)r << kRunOffBits;
     for (int t = t0; t < t1; t += 4) {
-      // four loads in flight before the first is consumed
       Rec16 rr[4];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) rr[j] = rec[t + j < t1 ? t + j : t0];
+      for (int j = 0; j < 4; ++j) rr[j] = fetch(t + j < t1 ? t + j : t0);
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const float dx = rr[j].x - qf[0], dy = rr[j].y - qf[1], dz = rr[j].z - qf[2];
         const float d2 = __builtin_fmaf(dz, dz, __builtin_fmaf(dy, dy, dx * dx));
-        uint32_t kk = (__float_as_uint(d2) & ~kKeyMask) | (uint32_t)((lid + j) & kKeyMask);
+        uint32_t kk = (__float_as_uint(d2) & ~kKeyMask) |
+                      rid | ((uint32_t)(t + j - t0) & ((1u << kRunOffBits) - 1));
         // inf / NaN: never a neighbour; past the run end: padding
         if (!(d2 <= 3.0e38f) || t + j >= t1) kk = kNoKey;
 #pragma unroll
         for (int s = K; s > 0; --s) key[s] = umed3(key[s - 1], key[s], kk);
         key[0] = min(key[0], kk);
       }
-      lid += min(4, t1 - t);
     }
   }
   // anything outside the 3x3x3 block is at least L away
@@ -1089,7 +1100,7 @@ __global__ __launch_bounds__(256) void k_knn(
     const double err = V * 0x1p-20 + 4.0 * dl * __builtin_sqrt(V) + 4.0 * dl * dl;
     B = fmin(B, V - err);
   }
-  bool ok = lid <= (int)(kKeyMask + 1) && Dq < 1e17;
+  bool ok = !overflow && Dq < 1e17;
   double ed[KL], e2[KL];
   int ei[KL];
 #pragma unroll
@@ -1099,11 +1110,9 @@ __global__ __launch_bounds__(256) void k_knn(
     ei[s] = -1;
     if (key[s] != kNoKey) {
       const int l = (int)(key[s] & kKeyMask);
-      int t = 0;
-#pragma unroll
-      for (int r = 0; r < 9; ++r)
-        if (rl[r] <= l) t = rb[r] + (l - rl[r]);
-      const int id = rec[t].idx;
+      int t0, t1;
+      runs(l >> kRunOffBits, t0, t1);
+      const int id = fetch(t0 + (l & ((1 << kRunOffBits) - 1))).idx;
       const double *tp = tgt + 3 * (size_t)id;
       const double ddx = tp[0] - qv[0], ddy = tp[1] - qv[1], ddz = tp[2] - qv[2];
       const double dsq = ddx * ddx + ddy * ddy + ddz * ddz;  // utils/kdtree.c:16
@@ -1112,7 +1121,7 @@ __global__ __launch_bounds__(256) void k_knn(
       ei[s] = id;
     }
   }
-  // insertion sort by (distance, index); f32 order is almost always right
+  // insertion sort by (distance, index); the f32 order is almost always right
 #pragma unroll
   for (int s = 1; s < KL; ++s) {
 #pragma unroll
@@ -1133,24 +1142,160 @@ __global__ __launch_bounds__(256) void k_knn(
     ok = ok && B > dk2 * (1.0 + 0x1p-48);
   else
     ok = ok && B == INFINITY;  // fewer than K neighbours: only if all was seen
-  double kd[K];
-  int ki[K];
   if (ok) {
 #pragma unroll
     for (int s = 0; s < K; ++s) {
-      kd[s] = ed[s];
-      ki[s] = ei[s];
+      oidx[q * K + s] = ei[s];
+      odist[q * K + s] = ed[s];
     }
   } else {
-    if (nslow) atomicAdd(nslow, 1ull);
-    // K listed points have dsq <= dk2: a valid starting bound
-    const double thr0 = dk2 < INFINITY ? dk2 * (1.0 + 0x1p-48) : INFINITY;
-    knn_exact_lane<K>(G, start, rec, tgt, qv, qf, dl, thr0, kd, ki);
+    // K listed points have dsq <= dk2: a valid starting bound for the slow
+    // path, which runs in its own launch (k_knn_slow) so its registers do not
+    // weigh on this one
+    const int e = atomicAdd(L_.n_slow, 1);
+    L_.slow_q[e] = (int)q;
+    L_.slow_thr[e] = dk2 < INFINITY ? dk2 * (1.0 + 0x1p-48) : INFINITY;
   }
+}
+
+constexpr int kTileThreads = 256;
+constexpr int kTileRec = 2048;  // records staged per tile: 32 KiB of LDS
+constexpr int kTileMaxW = 64;   // cells per tile along x
+
+// Global-mode exact k-NN over tiles of W consecutive cells of one grid row.
+// A tile stages the 9 neighbouring row segments (cells xa-1 .. xb+1) of the
+// cell-sorted target records into LDS with coalesced loads, then its threads
+// run the tile's (cell-sorted) queries against LDS. Tiles are dealt to the
+// 8 XCDs in contiguous ranges (block b runs on XCD b % 8 under the observed
+// round-robin placement; a different placement only costs L2 hits), so each
+// XCD's L2 holds only its slab of the cloud.
+// GLOBAL = false: the tile pass; a tile whose segments exceed the LDS budget
+// is appended to the overflow list. GLOBAL = true: the overflow tiles, read
+// straight from the global record array.
+template <int K, bool GLOBAL>
+__global__ __launch_bounds__(kTileThreads) void k_knn(
+    const GridParams *__restrict__ gp, const int *__restrict__ start,
+    const Rec16 *__restrict__ rec, const double *__restrict__ tgt,
+    const double *__restrict__ qs, const int *__restrict__ qstart,
+    const int *__restrict__ qperm, int32_t *__restrict__ oidx,
+    double *__restrict__ odist, KnnLists L_) {
+  __shared__ __attribute__((aligned(16))) Rec16 srec[GLOBAL ? 1 : kTileRec];
+  __shared__ int soff[9][kTileMaxW + 4];
+  __shared__ int sbase[10];
+  const GridParams G = *gp;
+  const int W = G.tile_w;
+  const int tpr = (G.g[0] + W - 1) / W;
+  long long t_lo, t_hi, step, first;
+  if (GLOBAL) {
+    t_lo = 0;
+    t_hi = *L_.n_ovf;
+    first = blockIdx.x;
+    step = gridDim.x;
+  } else {
+    const long long ntiles = (long long)tpr * G.g[1] * G.g[2];
+    const int xcd = blockIdx.x & 7;
+    t_lo = ntiles * xcd / 8;
+    t_hi = ntiles * (xcd + 1) / 8;
+    first = t_lo + (blockIdx.x >> 3);
+    step = gridDim.x >> 3;
+  }
+  for (long long it = first; it < t_hi; it += step) {
+    const long long tile = GLOBAL ? (long long)L_.ovf_tiles[it] : it;
+    const int row = (int)(tile / tpr), chunk = (int)(tile % tpr);
+    const int y = row % G.g[1], z = row / G.g[1];
+    const int xa = chunk * W, xb = min(xa + W, G.g[0]) - 1;
+    const int ncell = xb - xa + 4;  // soff[r][i] = first record of cell xa-1+i
+    for (int e = threadIdx.x; e < 9 * ncell; e += blockDim.x) {
+      const int r = e / ncell, i = e % ncell;
+      int dy, dz;
+      run_dydz(r, dy, dz);
+      const int yy = y + dy, zz = z + dz;
+      int v = 0;
+      if (yy >= 0 && yy < G.g[1] && zz >= 0 && zz < G.g[2]) {
+        const int x = min(max(xa - 1 + i, 0), G.g[0]);  // x = gx: row end
+        v = start[(zz * G.g[1] + yy) * G.g[0] + x];
+      }
+      soff[r][i] = v;
+    }
+    __syncthreads();
+    if (!GLOBAL) {
+      if (threadIdx.x == 0) {
+        int acc = 0;
+        for (int r = 0; r < 9; ++r) {
+          sbase[r] = acc;
+          acc += soff[r][ncell - 1] - soff[r][0];
+        }
+        sbase[9] = acc;
+      }
+      __syncthreads();
+      const int total = sbase[9];
+      if (total > kTileRec) {  // uniform: defer the tile to the global pass
+        if (threadIdx.x == 0) L_.ovf_tiles[atomicAdd(L_.n_ovf, 1)] = (int)tile;
+        __syncthreads();
+        continue;
+      }
+      for (int e = threadIdx.x; e < total; e += blockDim.x) {
+        int r = 0;
 #pragma unroll
-  for (int s = 0; s < K; ++s) {
-    oidx[q * K + s] = ki[s];
-    odist[q * K + s] = kd[s];
+        for (int u = 1; u < 9; ++u) r += e >= sbase[u] ? 1 : 0;
+        srec[e] = rec[soff[r][0] + (e - sbase[r])];
+      }
+      __syncthreads();
+    }
+    const int cell0 = (z * G.g[1] + y) * G.g[0];
+    const int q0 = qstart[cell0 + xa], q1 = qstart[cell0 + xb + 1];
+    for (int qi = q0 + threadIdx.x; qi < q1; qi += blockDim.x) {
+      const size_t q = (size_t)qperm[qi];
+      const double qv[3] = {qs[3 * q], qs[3 * q + 1], qs[3 * q + 2]};
+      const int c[3] = {cell_axis(qv[0], G, 0), y, z};
+      const int i = c[0] - xa;
+      if (!GLOBAL) {
+        knn_one<K>(G, tgt, qv, c, q,
+                   [&](int r, int &t0, int &t1) {
+                     const int sh = sbase[r] - soff[r][0];
+                     t0 = soff[r][i] + sh;
+                     t1 = soff[r][i + 3] + sh;
+                   },
+                   [&](int p) { return srec[p]; }, oidx, odist, L_);
+      } else {
+        knn_one<K>(G, tgt, qv, c, q,
+                   [&](int r, int &t0, int &t1) {
+                     t0 = soff[r][i];
+                     t1 = soff[r][i + 3];
+                   },
+                   [&](int p) { return rec[p]; }, oidx, odist, L_);
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// The queries k_knn could not certify: exact ring search from the recorded
+// starting bound.
+template <int K>
+__global__ __launch_bounds__(256) void k_knn_slow(
+    const GridParams *__restrict__ gp, const int *__restrict__ start,
+    const Rec16 *__restrict__ rec, const double *__restrict__ tgt,
+    const double *__restrict__ qs, int32_t *__restrict__ oidx,
+    double *__restrict__ odist, KnnLists L_) {
+  const GridParams G = *gp;
+  const int n = *L_.n_slow;
+  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < n;
+       e += gridDim.x * blockDim.x) {
+    const size_t q = (size_t)L_.slow_q[e];
+    const double qv[3] = {qs[3 * q], qs[3 * q + 1], qs[3 * q + 2]};
+    const double qr[3] = {qv[0] - G.o[0], qv[1] - G.o[1], qv[2] - G.o[2]};
+    const float qf[3] = {(float)qr[0], (float)qr[1], (float)qr[2]};
+    const double Dq = fmax(G.emax + G.h,
+                           fmax(fabs(qr[0]), fmax(fabs(qr[1]), fabs(qr[2]))));
+    double kd[K];
+    int ki[K];
+    knn_exact_lane<K>(G, start, rec, tgt, qv, qf, Dq * 0x1p-21, L_.slow_thr[e], kd, ki);
+#pragma unroll
+    for (int s = 0; s < K; ++s) {
+      oidx[q * K + s] = ki[s];
+      odist[q * K + s] = kd[s];
+    }
   }
 }
 
@@ -1175,7 +1320,8 @@ namespace {
 
 enum Slot {
   kBBox = 1, kParams, kCnt, kStart, kBSum, kCellId, kSlotBuf, kRec, kTan,
-  kKdFc, kKdP, kKdT, kQStart, kQCell, kQSlot, kQPerm, kStats,
+  kKdFc, kKdP, kKdT, kQStart, kQCell, kQSlot, kQPerm, kStats, kOvf, kSlowQ,
+  kSlowThr,
   kH0 = 100, kH1, kH2, kH3, kH4, kH5,
 };
 
@@ -1400,12 +1546,13 @@ double navgpu_timing_read(navgpu_ctx *ctx, const char *name, int reset) {
 }
 
 long long navgpu_knn_fallbacks(navgpu_ctx *ctx) {
-  if (!ctx || !ctx->knn_stats) return -1;
+  if (!ctx) return -1;
   auto it = ctx->bufs.find(kStats);
   if (it == ctx->bufs.end() || !it->second.first) return -1;
-  unsigned long long v = 0;
-  if (hipMemcpy(&v, it->second.first, 8, hipMemcpyDeviceToHost) != hipSuccess) return -1;
-  return (long long)v;
+  int v[2] = {0, 0};
+  if (hipStreamSynchronize(ctx->stream) != hipSuccess) return -1;
+  if (hipMemcpy(v, it->second.first, 8, hipMemcpyDeviceToHost) != hipSuccess) return -1;
+  return (long long)v[1];
 }
 
 int navgpu_timing_count(navgpu_ctx *ctx, const char *name) {
@@ -1737,7 +1884,7 @@ int navgpu_knn_dev(navgpu_ctx *ctx, const double *tgt, size_t nt,
       CHECK_LAUNCH("k_bbox_partial");
     }
     hipLaunchKernelGGL(k_grid_params, dim3(1), dim3(256), 0, s, part, nt ? nparts : 0,
-                       nt, cap, occ, gp);
+                       nt, cap, occ, nq, gp);
     CHECK_LAUNCH("k_grid_params");
     if (nt) {
       hipLaunchKernelGGL(k_cell_count, dim3(grid1d(nt, 256)), dim3(256), 0, s, tgt, nt,
@@ -1767,17 +1914,28 @@ int navgpu_knn_dev(navgpu_ctx *ctx, const double *tgt, size_t nt,
                        qcell, qslot, qstart, qperm);
     CHECK_LAUNCH("k_scatter_queries");
   }
-  unsigned long long *nslow = nullptr;
-  if (ctx->knn_stats) {
-    RC(ws(ctx, kStats, 1, &nslow));
-    HIP_TRY(hipMemsetAsync(nslow, 0, 8, s));
-  }
+  KnnLists lists;
+  int *counters;
+  RC(ws(ctx, kStats, 4, &counters));  // [n_ovf, n_slow, pad, pad]
+  RC(ws(ctx, kOvf, (size_t)cap + 1, &lists.ovf_tiles));
+  RC(ws(ctx, kSlowQ, nq, &lists.slow_q));
+  RC(ws(ctx, kSlowThr, nq, &lists.slow_thr));
+  lists.n_ovf = counters;
+  lists.n_slow = counters + 1;
+  HIP_TRY(hipMemsetAsync(counters, 0, 16, s));
   TimedRegion tr(ctx, "knn_query");
-  const dim3 g(grid1d(nq, 256)), b(256);
-#define KNN_CASE(KK)                                                            \
-  case KK:                                                                      \
-    hipLaunchKernelGGL(k_knn<KK>, g, b, 0, s, gp, tstart, rec, tgt, queries,   \
-                       qperm, nq, idx, dist, nslow);                            \
+  // tiles are walked by a grid of 8 x nbx blocks (block b -> XCD b % 8)
+  const int nbx = (int)std::min<size_t>(256, std::max<size_t>(1, nq / 1600 + 1));
+  const dim3 g(8 * nbx), b(kTileThreads);
+  const dim3 gs(std::max<unsigned>(1, std::min<unsigned>(1024, grid1d(nq, 256))));
+#define KNN_CASE(KK)                                                              \
+  case KK:                                                                        \
+    hipLaunchKernelGGL((k_knn<KK, false>), g, b, 0, s, gp, tstart, rec, tgt,     \
+                       queries, qstart, qperm, idx, dist, lists);                 \
+    hipLaunchKernelGGL((k_knn<KK, true>), g, b, 0, s, gp, tstart, rec, tgt,      \
+                       queries, qstart, qperm, idx, dist, lists);                 \
+    hipLaunchKernelGGL((k_knn_slow<KK>), gs, dim3(256), 0, s, gp, tstart, rec,    \
+                       tgt, queries, idx, dist, lists);                           \
     break;
   switch (k) {
     KNN_CASE(1)
