@@ -672,8 +672,7 @@ struct __align__(16) Rec16 {  // cell-sorted target: (coords - origin) in f32
 };
 
 constexpr int kBBoxBlocks = 1024;
-constexpr int kKeyBits = 11;  // local id in the low bits of a key: run (4) | offset (7)
-constexpr int kRunOffBits = 7;
+constexpr int kKeyBits = 10;  // local id in the low bits of a key: cell (5) | offset (5)
 constexpr uint32_t kKeyMask = (1u << kKeyBits) - 1;
 constexpr uint32_t kNoKey = 0xffffffffu;
 
@@ -919,92 +918,6 @@ __device__ __forceinline__ float f32_bound(double T, double dl) {
   return (float)((T + E) * (1.0 + 0x1p-20));
 }
 
-// Exact k-NN of one query by expanding Chebyshev rings of cells: reference
-// distance in f64, (distance, index) ordering, stops when nothing outside the
-// visited block can still enter. thr0 is an upper bound on the K-th best dsq
-// (x (1 + 2^-48)) known beforehand (INFINITY if none); an f32 distance on the
-// cell-sorted records screens every candidate before its f64 coordinates are
-// loaded. The slow path of k_knn: near ties the fast path cannot certify,
-// and queries whose neighbourhood reaches past the 3x3x3 block.
-template <int K>
-__device__ void knn_exact_lane(const GridParams &G, const int *__restrict__ start,
-                               const Rec16 *__restrict__ rec,
-                               const double *__restrict__ tgt, const double *qv,
-                               const float *qf, double dl, double thr0,
-                               double *kd, int *ki) {
-#pragma unroll
-  for (int s = 0; s < K; ++s) {
-    kd[s] = INFINITY;
-    ki[s] = -1;
-  }
-  double thr = thr0;
-  float thr_f = f32_bound(thr, dl);
-  const int c[3] = {cell_axis(qv[0], G, 0), cell_axis(qv[1], G, 1),
-                    cell_axis(qv[2], G, 2)};
-  const int gmax = max(G.g[0], max(G.g[1], G.g[2]));
-  for (int r = 0; r <= gmax; ++r) {
-    for (int dz = -r; dz <= r; ++dz) {
-      const int z = c[2] + dz;
-      if (z < 0 || z >= G.g[2]) continue;
-      for (int dy = -r; dy <= r; ++dy) {
-        const int y = c[1] + dy;
-        if (y < 0 || y >= G.g[1]) continue;
-        const bool face = (dz == -r || dz == r || dy == -r || dy == r);
-        const int step = (face || r == 0) ? 1 : 2 * r;
-        for (int dx = -r; dx <= r; dx += step) {
-          const int x = c[0] + dx;
-          if (x < 0 || x >= G.g[0]) continue;
-          if (box_d2(G, qv, x, x, y, y, z, z) > thr) continue;
-          const int cell = (z * G.g[1] + y) * G.g[0] + x;
-          const int b = start[cell], e = start[cell + 1];
-          for (int t = b; t < e; ++t) {
-            const Rec16 rr = rec[t];
-            const float fx = rr.x - qf[0], fy = rr.y - qf[1], fz = rr.z - qf[2];
-            const float d2f = __builtin_fmaf(fz, fz, __builtin_fmaf(fy, fy, fx * fx));
-            if (!(d2f <= thr_f)) continue;
-            const int id = rr.idx;
-            const double *tp = tgt + 3 * (size_t)id;
-            const double ddx = tp[0] - qv[0], ddy = tp[1] - qv[1], ddz = tp[2] - qv[2];
-            const double dsq = ddx * ddx + ddy * ddy + ddz * ddz;
-            if (!(dsq <= thr)) continue;
-            const double d = __builtin_sqrt(dsq);
-            if (!knn_less(d, id, kd[K - 1], ki[K - 1])) continue;
-            bool placed = false;
-#pragma unroll
-            for (int s = K - 1; s >= 0; --s) {
-              if (!placed) {
-                if (s > 0 && knn_less(d, id, kd[s - 1], ki[s - 1])) {
-                  kd[s] = kd[s - 1];
-                  ki[s] = ki[s - 1];
-                } else {
-                  kd[s] = d;
-                  ki[s] = id;
-                  placed = true;
-                }
-              }
-            }
-            const double w = kd[K - 1];
-            if (w < INFINITY) {
-              thr = fmin(thr, w * w * (1.0 + 0x1p-48));
-              thr_f = f32_bound(thr, dl);
-            }
-          }
-        }
-      }
-    }
-    double L = INFINITY;
-#pragma unroll
-    for (int a = 0; a < 3; ++a) {
-      if (c[a] - r > 0) L = fmin(L, qv[a] - (G.o[a] + (c[a] - r) * G.h));
-      if (c[a] + r < G.g[a] - 1) L = fmin(L, (G.o[a] + (c[a] + r + 1) * G.h) - qv[a]);
-    }
-    if (L == INFINITY) break;
-    const double Lg = L - 2.0 * G.delta;
-    // every point with dsq <= thr lies inside the visited block
-    if (Lg > 0.0 && thr < Lg * Lg) break;
-  }
-}
-
 __device__ __forceinline__ uint32_t umed3(uint32_t a, uint32_t b, uint32_t c) {
   return max(min(a, b), min(max(a, b), c));
 }
@@ -1016,67 +929,95 @@ __device__ __forceinline__ void run_dydz(int r, int &dy, int &dz) {
 }
 
 // One query of the global-mode k-NN.
-// Fast path: the 9 x-runs of the query's 3x3x3 neighbourhood, [rb[r], re[r])
-// in the index space of `fetch` (LDS tile or global array), centre run first;
-// a run whose cell box is already beyond the current (K+1)-th candidate is
-// skipped. Each candidate gets an f32 distance packed with its local id into a
-// 32-bit key; a sorted list of K+1 keys is kept by branch-free median-of-3
-// insertion. The K+1 survivors are then re-evaluated with the reference f64
-// formula and sorted by (distance, index); the result is certified exact when
-// every candidate left out (visited but not kept, skipped, or outside the
-// block) is provably farther than the K-th, using the f32 error bound.
-// Otherwise (near ties, sparse cells, lid overflow) the lane runs
-// knn_exact_lane over the global arrays.
+// Fast path over the query's 3x3x3 cell neighbourhood, own cell first, then
+// faces, edges, corners; a cell whose box is already beyond the current
+// (K+1)-th candidate is skipped. Each candidate gets an f32 distance
+// (coordinates relative to the grid origin) packed with its local id
+// (cell slot | offset) into a 32-bit key; a sorted list of the K+1 smallest
+// keys is kept by branch-free median-of-3 insertion. The K+1 survivors are
+// then re-evaluated with the reference f64 formula and ordered by
+// (distance, index); the result is certified exact when every candidate left
+// out (visited but not kept, skipped, or outside the block) is provably
+// farther than the K-th, using the f32 error bound. Otherwise (near ties, a
+// neighbourhood reaching past the block, overfull cells) the query is queued
+// for k_knn_slow with the K-th distance found as its starting bound.
+// cells(r, dx, t0, t1): record range of cell x+dx in run r, in the index space
+// of fetch (LDS tile or global array).
+__constant__ signed char kCellRun[27] = {0, 0, 0, 1, 2, 3, 4, 1, 1, 2, 2, 3, 3, 4,
+                                         4, 5, 6, 7, 8, 5, 5, 6, 6, 7, 7, 8, 8};
+__constant__ signed char kCellDx[27] = {0, -1, 1, 0, 0, 0, 0, -1, 1, -1, 1, -1, 1, -1,
+                                        1, 0, 0, 0, 0, -1, 1, -1, 1, -1, 1, -1, 1};
+constexpr int kCellOffBits = 5;  // candidates per cell slot in a key
+
 struct KnnLists {
   int *ovf_tiles, *n_ovf;  // tiles whose segments overflow the LDS budget
   int *slow_q, *n_slow;    // queries the fast path could not certify
   double *slow_thr;        // their starting bound (K-th dsq upper bound)
 };
 
-template <int K, class Runs, class Fetch>
+template <int K, class Cells, class Fetch>
 __device__ __forceinline__ void knn_one(
     const GridParams &G, const double *__restrict__ tgt, const double qv[3],
-    const int c[3], size_t q, Runs runs, Fetch fetch,
+    const int c[3], size_t q, Cells cells, Fetch fetch,
     int32_t *__restrict__ oidx, double *__restrict__ odist, const KnnLists &L_) {
   const double qr[3] = {qv[0] - G.o[0], qv[1] - G.o[1], qv[2] - G.o[2]};
   const float qf[3] = {(float)qr[0], (float)qr[1], (float)qr[2]};
-  // |f32 coordinate difference - exact difference| <= dl: both operands
-  // rounded to f32 once (relative 2^-24), then one f32 subtraction
+  // |f32 difference - exact difference| <= dl: each operand rounded to f32
+  // once (<= 2^-24 |v| each), one f32 subtraction (<= 2^-24 |difference|)
   const double Dq = fmax(G.emax + G.h,
                          fmax(fabs(qr[0]), fmax(fabs(qr[1]), fabs(qr[2]))));
-  const double dl = Dq * 0x1p-21;
+  const double dl = Dq * 0x1p-22;
+  // per-axis lower bounds on the distance to the cells at offsets -1, 0, +1
+  // (shrunk by the f32 slack), squared: a cell's box bound is a sum of three
+  float e2v[3][3];
+#pragma unroll
+  for (int a = 0; a < 3; ++a) {
+    const double lo = c[a] * G.h, hi = (c[a] + 1) * G.h;
+    const double m = 2.0 * dl + 2.0 * G.delta;
+    const double dm = fmax(0.0, qr[a] - lo - m);
+    const double dp = fmax(0.0, hi - qr[a] - m);
+    const double d0 = fmax(0.0, fmax(c[a] > 0 ? lo - qr[a] : 0.0,
+                                     c[a] < G.g[a] - 1 ? qr[a] - hi : 0.0) - m);
+    const float fm = (float)dm * (1.0f - 0x1p-20f), f0 = (float)d0 * (1.0f - 0x1p-20f),
+                fp = (float)dp * (1.0f - 0x1p-20f);
+    e2v[a][0] = fm * fm;
+    e2v[a][1] = f0 * f0;
+    e2v[a][2] = fp * fp;
+  }
   constexpr int KL = K + 1;
   uint32_t key[KL];
 #pragma unroll
   for (int s = 0; s < KL; ++s) key[s] = kNoKey;
-  bool overflow = false;  // a run longer than 2^kRunOffBits candidates
-  const int x0 = max(c[0] - 1, 0), x1 = min(c[0] + 1, G.g[0] - 1);
+  bool overflow = false;  // a cell with more than 2^kCellOffBits candidates
 #pragma unroll 1
-  for (int r = 0; r < 9; ++r) {
+  for (int ci = 0; ci < 27; ++ci) {
+    const int r = kCellRun[ci], dx = kCellDx[ci];
     int t0, t1;
-    runs(r, t0, t1);
+    cells(r, dx, t0, t1);
     if (t0 >= t1) continue;
-    if (r > 0 && key[K] != kNoKey) {
+    if (ci > 0 && key[K] != kNoKey) {
       int dyv, dzv;
       run_dydz(r, dyv, dzv);
-      const double V = (double)__uint_as_float(key[K] & ~kKeyMask);
-      if (box_d2(G, qv, x0, x1, c[1] + dyv, c[1] + dyv, c[2] + dzv, c[2] + dzv) > V)
-        continue;
+      const float bx = dx < 0 ? e2v[0][0] : (dx > 0 ? e2v[0][2] : e2v[0][1]);
+      const float by = dyv < 0 ? e2v[1][0] : (dyv > 0 ? e2v[1][2] : e2v[1][1]);
+      const float bz = dzv < 0 ? e2v[2][0] : (dzv > 0 ? e2v[2][2] : e2v[2][1]);
+      const float bd2 = (bx + by) + bz;
+      if (bd2 * (1.0f - 0x1p-20f) > __uint_as_float(key[K] & ~kKeyMask)) continue;
     }
-    overflow |= (t1 - t0) > (1 << kRunOffBits);
-    const uint32_t rid = (uint32_t)r << kRunOffBits;
-    for (int t = t0; t < t1; t += 4) {
-      Rec16 rr[4];
+    overflow |= (t1 - t0) > (1 << kCellOffBits);
+    const uint32_t cid = (uint32_t)ci << kCellOffBits;
+    for (int t = t0; t < t1; t += 2) {
+      Rec16 rp[2];
+      rp[0] = fetch(t);
+      rp[1] = fetch(t + 1 < t1 ? t + 1 : t);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) rr[j] = fetch(t + j < t1 ? t + j : t0);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const float dx = rr[j].x - qf[0], dy = rr[j].y - qf[1], dz = rr[j].z - qf[2];
-        const float d2 = __builtin_fmaf(dz, dz, __builtin_fmaf(dy, dy, dx * dx));
-        uint32_t kk = (__float_as_uint(d2) & ~kKeyMask) |
-                      rid | ((uint32_t)(t + j - t0) & ((1u << kRunOffBits) - 1));
-        // inf / NaN: never a neighbour; past the run end: padding
-        if (!(d2 <= 3.0e38f) || t + j >= t1) kk = kNoKey;
+      for (int j = 0; j < 2; ++j) {
+        const Rec16 rr = rp[j];
+        const float fx = rr.x - qf[0], fy = rr.y - qf[1], fz = rr.z - qf[2];
+        const float d2 = __builtin_fmaf(fz, fz, __builtin_fmaf(fy, fy, fx * fx));
+        uint32_t kk = (__float_as_uint(d2) & ~kKeyMask) | cid |
+                      ((uint32_t)(t + j - t0) & ((1u << kCellOffBits) - 1));
+        if (j && t + 1 >= t1) kk = kNoKey;  // padding past the cell end
 #pragma unroll
         for (int s = K; s > 0; --s) key[s] = umed3(key[s - 1], key[s], kk);
         key[0] = min(key[0], kk);
@@ -1101,45 +1042,54 @@ __device__ __forceinline__ void knn_one(
     B = fmin(B, V - err);
   }
   bool ok = !overflow && Dq < 1e17;
-  double ed[KL], e2[KL];
+  double ed[KL];
   int ei[KL];
 #pragma unroll
   for (int s = 0; s < KL; ++s) {
     ed[s] = INFINITY;
-    e2[s] = INFINITY;
     ei[s] = -1;
     if (key[s] != kNoKey) {
       const int l = (int)(key[s] & kKeyMask);
+      const int ci = l >> kCellOffBits;
       int t0, t1;
-      runs(l >> kRunOffBits, t0, t1);
-      const int id = fetch(t0 + (l & ((1 << kRunOffBits) - 1))).idx;
+      cells(kCellRun[ci], kCellDx[ci], t0, t1);
+      const int id = fetch(t0 + (l & ((1 << kCellOffBits) - 1))).idx;
       const double *tp = tgt + 3 * (size_t)id;
       const double ddx = tp[0] - qv[0], ddy = tp[1] - qv[1], ddz = tp[2] - qv[2];
       const double dsq = ddx * ddx + ddy * ddy + ddz * ddz;  // utils/kdtree.c:16
-      e2[s] = dsq;
       ed[s] = __builtin_sqrt(dsq);
       ei[s] = id;
+      // an inf/NaN distance is never a neighbour (kdtree.c:117)
+      if (!(ed[s] < INFINITY)) {
+        ed[s] = INFINITY;
+        ei[s] = -1;
+        ok = false;
+      }
     }
   }
-  // insertion sort by (distance, index); the f32 order is almost always right
+  // order by (distance, index): the f32 order is almost always already right
+  bool sorted = true;
 #pragma unroll
-  for (int s = 1; s < KL; ++s) {
+  for (int s = 1; s < KL; ++s) sorted &= !knn_less(ed[s], ei[s], ed[s - 1], ei[s - 1]);
+  if (!sorted) {  // rare: bubble passes (a fixed-trip loop keeps VGPRs low)
+#pragma unroll 1
+    for (int pass = 0; pass < KL - 1; ++pass) {
 #pragma unroll
-    for (int u = s; u > 0; --u) {
-      const bool sw = knn_less(ed[u], ei[u], ed[u - 1], ei[u - 1]);
-      const double td = ed[u], t2 = e2[u];
-      const int ti = ei[u];
-      ed[u] = sw ? ed[u - 1] : ed[u];
-      e2[u] = sw ? e2[u - 1] : e2[u];
-      ei[u] = sw ? ei[u - 1] : ei[u];
-      ed[u - 1] = sw ? td : ed[u - 1];
-      e2[u - 1] = sw ? t2 : e2[u - 1];
-      ei[u - 1] = sw ? ti : ei[u - 1];
+      for (int u = 1; u < KL; ++u) {
+        const bool sw = knn_less(ed[u], ei[u], ed[u - 1], ei[u - 1]);
+        const double td = ed[u];
+        const int ti = ei[u];
+        ed[u] = sw ? ed[u - 1] : ed[u];
+        ei[u] = sw ? ei[u - 1] : ei[u];
+        ed[u - 1] = sw ? td : ed[u - 1];
+        ei[u - 1] = sw ? ti : ei[u - 1];
+      }
     }
   }
-  const double dk2 = e2[K - 1];
-  if (dk2 < INFINITY)
-    ok = ok && B > dk2 * (1.0 + 0x1p-48);
+  const double dk = ed[K - 1];
+  const double dk2 = dk * dk;  // >= the exact K-th dsq (sqrt rounds to nearest)
+  if (dk < INFINITY)
+    ok = ok && B > dk2 * (1.0 + 0x1p-46);
   else
     ok = ok && B == INFINITY;  // fewer than K neighbours: only if all was seen
   if (ok) {
@@ -1150,11 +1100,10 @@ __device__ __forceinline__ void knn_one(
     }
   } else {
     // K listed points have dsq <= dk2: a valid starting bound for the slow
-    // path, which runs in its own launch (k_knn_slow) so its registers do not
-    // weigh on this one
+    // path, which runs in its own launch (k_knn_slow)
     const int e = atomicAdd(L_.n_slow, 1);
     L_.slow_q[e] = (int)q;
-    L_.slow_thr[e] = dk2 < INFINITY ? dk2 * (1.0 + 0x1p-48) : INFINITY;
+    L_.slow_thr[e] = dk < INFINITY ? dk2 * (1.0 + 0x1p-46) : INFINITY;
   }
 }
 
@@ -1251,17 +1200,17 @@ __global__ __launch_bounds__(kTileThreads) void k_knn(
       const int i = c[0] - xa;
       if (!GLOBAL) {
         knn_one<K>(G, tgt, qv, c, q,
-                   [&](int r, int &t0, int &t1) {
+                   [&](int r, int dx, int &t0, int &t1) {
                      const int sh = sbase[r] - soff[r][0];
-                     t0 = soff[r][i] + sh;
-                     t1 = soff[r][i + 3] + sh;
+                     t0 = soff[r][i + 1 + dx] + sh;
+                     t1 = soff[r][i + 2 + dx] + sh;
                    },
                    [&](int p) { return srec[p]; }, oidx, odist, L_);
       } else {
         knn_one<K>(G, tgt, qv, c, q,
-                   [&](int r, int &t0, int &t1) {
-                     t0 = soff[r][i];
-                     t1 = soff[r][i + 3];
+                   [&](int r, int dx, int &t0, int &t1) {
+                     t0 = soff[r][i + 1 + dx];
+                     t1 = soff[r][i + 2 + dx];
                    },
                    [&](int p) { return rec[p]; }, oidx, odist, L_);
       }
@@ -1270,8 +1219,31 @@ __global__ __launch_bounds__(kTileThreads) void k_knn(
   }
 }
 
-// The queries k_knn could not certify: exact ring search from the recorded
-// starting bound.
+// insert (d, id) into the sorted exact list kd/ki if it ranks among the K
+template <int K>
+__device__ __forceinline__ void knn_insert(double *kd, int *ki, double d, int id) {
+  if (!knn_less(d, id, kd[K - 1], ki[K - 1])) return;
+  bool placed = false;
+#pragma unroll
+  for (int s = K - 1; s >= 0; --s) {
+    if (!placed) {
+      if (s > 0 && knn_less(d, id, kd[s - 1], ki[s - 1])) {
+        kd[s] = kd[s - 1];
+        ki[s] = ki[s - 1];
+      } else {
+        kd[s] = d;
+        ki[s] = id;
+        placed = true;
+      }
+    }
+  }
+}
+
+// The queries k_knn could not certify, one WAVE per query: exact ring search
+// from the recorded starting bound. Each ring's cells are split over the 64
+// lanes (f32 screen, then the reference f64 distance), each lane keeps its
+// own sorted list, and after every ring the lists are merged by K rounds of a
+// 64-lane (distance, index) argmin; the merged K-th bounds the next ring.
 template <int K>
 __global__ __launch_bounds__(256) void k_knn_slow(
     const GridParams *__restrict__ gp, const int *__restrict__ start,
@@ -1280,21 +1252,104 @@ __global__ __launch_bounds__(256) void k_knn_slow(
     double *__restrict__ odist, KnnLists L_) {
   const GridParams G = *gp;
   const int n = *L_.n_slow;
-  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < n;
-       e += gridDim.x * blockDim.x) {
+  const int lane = threadIdx.x & (kWave - 1);
+  const int wave = (int)((blockIdx.x * blockDim.x + threadIdx.x) / kWave);
+  const int nwaves = (int)(gridDim.x * blockDim.x / kWave);
+  const int gmax = max(G.g[0], max(G.g[1], G.g[2]));
+  for (int e = wave; e < n; e += nwaves) {
     const size_t q = (size_t)L_.slow_q[e];
+    double thr = L_.slow_thr[e];
     const double qv[3] = {qs[3 * q], qs[3 * q + 1], qs[3 * q + 2]};
     const double qr[3] = {qv[0] - G.o[0], qv[1] - G.o[1], qv[2] - G.o[2]};
     const float qf[3] = {(float)qr[0], (float)qr[1], (float)qr[2]};
     const double Dq = fmax(G.emax + G.h,
                            fmax(fabs(qr[0]), fmax(fabs(qr[1]), fabs(qr[2]))));
-    double kd[K];
-    int ki[K];
-    knn_exact_lane<K>(G, start, rec, tgt, qv, qf, Dq * 0x1p-21, L_.slow_thr[e], kd, ki);
+    const double dl = Dq * 0x1p-22;
+    float thr_f = f32_bound(thr, dl);
+    const int c[3] = {cell_axis(qv[0], G, 0), cell_axis(qv[1], G, 1),
+                      cell_axis(qv[2], G, 2)};
+    double kd[K], md[K];
+    int ki[K], mi[K];
 #pragma unroll
     for (int s = 0; s < K; ++s) {
-      oidx[q * K + s] = ki[s];
-      odist[q * K + s] = kd[s];
+      kd[s] = INFINITY;
+      ki[s] = -1;
+    }
+    for (int r = 0; r <= gmax; ++r) {
+      const int side = 2 * r + 1, ncube = side * side * side;
+      for (int u = lane; u < ncube; u += kWave) {
+        const int dz = u / (side * side) - r, dy = (u / side) % side - r, dx = u % side - r;
+        if (max(abs(dx), max(abs(dy), abs(dz))) != r) continue;  // earlier ring
+        const int x = c[0] + dx, y = c[1] + dy, z = c[2] + dz;
+        if (x < 0 || x >= G.g[0] || y < 0 || y >= G.g[1] || z < 0 || z >= G.g[2]) continue;
+        if (box_d2(G, qv, x, x, y, y, z, z) > thr) continue;
+        const int cell = (z * G.g[1] + y) * G.g[0] + x;
+        const int b = start[cell], en = start[cell + 1];
+        for (int t = b; t < en; ++t) {
+          const Rec16 rr = rec[t];
+          const float fx = rr.x - qf[0], fy = rr.y - qf[1], fz = rr.z - qf[2];
+          const float d2f = __builtin_fmaf(fz, fz, __builtin_fmaf(fy, fy, fx * fx));
+          if (!(d2f <= thr_f)) continue;
+          const double *tp = tgt + 3 * (size_t)rr.idx;
+          const double ddx = tp[0] - qv[0], ddy = tp[1] - qv[1], ddz = tp[2] - qv[2];
+          const double dsq = ddx * ddx + ddy * ddy + ddz * ddz;
+          if (!(dsq <= thr)) continue;
+          knn_insert<K>(kd, ki, __builtin_sqrt(dsq), rr.idx);
+        }
+      }
+      // merge the 64 lane lists: K rounds of a wave argmin on the list heads
+#pragma unroll
+      for (int s = 0; s < K; ++s) {
+        double bd = kd[0];
+        int bi = ki[0], bl = lane;
+#pragma unroll
+        for (int o = kWave / 2; o > 0; o >>= 1) {
+          const double od = __shfl_xor(bd, o, kWave);
+          const int oi = __shfl_xor(bi, o, kWave), ol = __shfl_xor(bl, o, kWave);
+          const bool take = knn_less(od, oi, bd, bi) ||
+                            (!knn_less(bd, bi, od, oi) && ol < bl);
+          bd = take ? od : bd;
+          bi = take ? oi : bi;
+          bl = take ? ol : bl;
+        }
+        md[s] = bd;
+        mi[s] = bi;
+        if (lane == bl) {  // pop the winner's head
+#pragma unroll
+          for (int u = 0; u < K - 1; ++u) {
+            kd[u] = kd[u + 1];
+            ki[u] = ki[u + 1];
+          }
+          kd[K - 1] = INFINITY;
+          ki[K - 1] = -1;
+        }
+      }
+      // lane 0 carries the merged list into the next ring
+#pragma unroll
+      for (int s = 0; s < K; ++s) {
+        kd[s] = lane == 0 ? md[s] : INFINITY;
+        ki[s] = lane == 0 ? mi[s] : -1;
+      }
+      if (md[K - 1] < INFINITY) {
+        thr = fmin(thr, md[K - 1] * md[K - 1] * (1.0 + 0x1p-46));
+        thr_f = f32_bound(thr, dl);
+      }
+      double L = INFINITY;
+#pragma unroll
+      for (int a = 0; a < 3; ++a) {
+        if (c[a] - r > 0) L = fmin(L, qv[a] - (G.o[a] + (c[a] - r) * G.h));
+        if (c[a] + r < G.g[a] - 1) L = fmin(L, (G.o[a] + (c[a] + r + 1) * G.h) - qv[a]);
+      }
+      if (L == INFINITY) break;
+      const double Lg = L - 2.0 * G.delta;
+      if (Lg > 0.0 && thr < Lg * Lg) break;  // all points with dsq <= thr seen
+    }
+    if (lane == 0) {
+#pragma unroll
+      for (int s = 0; s < K; ++s) {
+        oidx[q * K + s] = mi[s];
+        odist[q * K + s] = md[s];
+      }
     }
   }
 }
@@ -1927,7 +1982,7 @@ int navgpu_knn_dev(navgpu_ctx *ctx, const double *tgt, size_t nt,
   // tiles are walked by a grid of 8 x nbx blocks (block b -> XCD b % 8)
   const int nbx = (int)std::min<size_t>(256, std::max<size_t>(1, nq / 1600 + 1));
   const dim3 g(8 * nbx), b(kTileThreads);
-  const dim3 gs(std::max<unsigned>(1, std::min<unsigned>(1024, grid1d(nq, 256))));
+  const dim3 gs(std::max<unsigned>(1, std::min<unsigned>(2048, grid1d(nq, 256))));
 #define KNN_CASE(KK)                                                              \
   case KK:                                                                        \
     hipLaunchKernelGGL((k_knn<KK, false>), g, b, 0, s, gp, tstart, rec, tgt,     \
