@@ -1276,12 +1276,15 @@ __global__ __launch_bounds__(256) void k_knn_slow(
       ki[s] = -1;
     }
     for (int r = 0; r <= gmax; ++r) {
-      const int side = 2 * r + 1, ncube = side * side * side;
-      for (int u = lane; u < ncube; u += kWave) {
-        const int dz = u / (side * side) - r, dy = (u / side) % side - r, dx = u % side - r;
-        if (max(abs(dx), max(abs(dy), abs(dz))) != r) continue;  // earlier ring
-        const int x = c[0] + dx, y = c[1] + dy, z = c[2] + dz;
-        if (x < 0 || x >= G.g[0] || y < 0 || y >= G.g[1] || z < 0 || z >= G.g[2]) continue;
+      // the ring's cube clipped to the grid (a degenerate axis stays 1 thick)
+      const int xl = max(c[0] - r, 0), xh = min(c[0] + r, G.g[0] - 1);
+      const int yl = max(c[1] - r, 0), yh = min(c[1] + r, G.g[1] - 1);
+      const int zl = max(c[2] - r, 0), zh = min(c[2] + r, G.g[2] - 1);
+      const int bx = xh - xl + 1, by = yh - yl + 1, bz = zh - zl + 1;
+      const int nbox = bx * by * bz;
+      for (int u = lane; u < nbox; u += kWave) {
+        const int x = xl + u % bx, y = yl + (u / bx) % by, z = zl + u / (bx * by);
+        if (max(abs(x - c[0]), max(abs(y - c[1]), abs(z - c[2]))) != r) continue;
         if (box_d2(G, qv, x, x, y, y, z, z) > thr) continue;
         const int cell = (z * G.g[1] + y) * G.g[0] + x;
         const int b = start[cell], en = start[cell + 1];

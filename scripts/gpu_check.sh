@@ -19,7 +19,7 @@ step() {  # step <name> <timeout> cmd...
   return 0
 }
 step build 600 python3 -c "import __graft_entry__ as g; g.build()"
-step pytest 1500 python3 -m pytest tests -m gpu -q -x --timeout 600 "$@"
+step pytest 1500 python3 -u -m pytest tests -m gpu -v -x --timeout 240 --timeout-method=thread "$@"
 step smoke 300 python3 -c "import __graft_entry__ as g; g.smoke()"
 step bench 600 python3 bench.py --json-out "$OUT/bench.json"
 step bench_k2 300 python3 bench.py --workload k2 --steps 10 --json-out "$OUT/bench_k2.json"

@@ -3,7 +3,7 @@
 TAG=${1:-q}; shift; OUT=gpurun_out/$TAG; mkdir -p "$OUT"
 export NAVSLAM_QUIET=1
 fatal() { [ "$1" -ge 124 ] || [ "$1" -eq 134 ] || [ "$1" -eq 139 ]; }
-timeout -k 10 900 python3 -m pytest tests -m gpu -q -x --timeout 600 "$@" > "$OUT/pytest.log" 2>&1; rc=$?
+PYTHONUNBUFFERED=1 timeout -k 10 900 python3 -m pytest tests -m gpu -v -x --timeout 240 --timeout-method=thread "$@" > "$OUT/pytest.log" 2>&1; rc=$?
 echo "pytest rc=$rc"; tail -n 4 "$OUT/pytest.log"
 if fatal $rc; then exit $rc; fi
 for occ in ${OCCS:-5}; do
