@@ -666,6 +666,13 @@ struct GridParams {
   int tile_w;       // cells per k_knn tile along x
 };
 
+#ifndef NAVGPU_TILE_QUERIES
+#define NAVGPU_TILE_QUERIES 220.0  // target queries per k_knn tile
+#endif
+#ifndef NAVGPU_TILE_REC
+#define NAVGPU_TILE_REC 2048
+#endif
+
 struct __align__(16) Rec16 {  // cell-sorted target: (coords - origin) in f32
   float x, y, z;
   int idx;
@@ -777,7 +784,8 @@ __global__ __launch_bounds__(256) void k_grid_params(const double *__restrict__ 
   // tile width: ~220 queries per 256-thread tile, and its 9 staged row
   // segments of W+2 cells within ~90 % of the LDS record budget
   const double occ_q = (double)nq / G.ncells, occ_t = (double)n / G.ncells;
-  double w = fmin(220.0 / fmax(occ_q, 1e-9), 0.9 * 2048 / (9.0 * fmax(occ_t, 1e-9)) - 2.0);
+  double w = fmin(NAVGPU_TILE_QUERIES / fmax(occ_q, 1e-9),
+                  0.9 * NAVGPU_TILE_REC / (9.0 * fmax(occ_t, 1e-9)) - 2.0);
   G.tile_w = (int)fmax(1.0, fmin(64.0, floor(w)));
   *gp = G;
 }
@@ -1010,11 +1018,16 @@ __device__ __forceinline__ void knn_one(
       Rec16 rp[2];
       rp[0] = fetch(t);
       rp[1] = fetch(t + 1 < t1 ? t + 1 : t);
+      // the pair's f32 distances in packed math (v_pk_*_f32)
+      typedef float f2 __attribute__((ext_vector_type(2)));
+      const f2 px = {rp[0].x, rp[1].x}, py = {rp[0].y, rp[1].y}, pz = {rp[0].z, rp[1].z};
+      const f2 qx2 = {qf[0], qf[0]}, qy2 = {qf[1], qf[1]}, qz2 = {qf[2], qf[2]};
+      const f2 fx2 = px - qx2, fy2 = py - qy2, fz2 = pz - qz2;
+      const f2 d22 = __builtin_elementwise_fma(
+          fz2, fz2, __builtin_elementwise_fma(fy2, fy2, fx2 * fx2));
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
-        const Rec16 rr = rp[j];
-        const float fx = rr.x - qf[0], fy = rr.y - qf[1], fz = rr.z - qf[2];
-        const float d2 = __builtin_fmaf(fz, fz, __builtin_fmaf(fy, fy, fx * fx));
+        const float d2 = d22[j];
         uint32_t kk = (__float_as_uint(d2) & ~kKeyMask) | cid |
                       ((uint32_t)(t + j - t0) & ((1u << kCellOffBits) - 1));
         if (j && t + 1 >= t1) kk = kNoKey;  // padding past the cell end
@@ -1107,8 +1120,14 @@ __device__ __forceinline__ void knn_one(
   }
 }
 
-constexpr int kTileThreads = 256;
-constexpr int kTileRec = 2048;  // records staged per tile: 32 KiB of LDS
+#ifndef NAVGPU_TILE_THREADS
+#define NAVGPU_TILE_THREADS 256
+#endif
+#ifndef NAVGPU_TILE_REC
+#define NAVGPU_TILE_REC 2048
+#endif
+constexpr int kTileThreads = NAVGPU_TILE_THREADS;
+constexpr int kTileRec = NAVGPU_TILE_REC;  // records staged per tile (16 B each)
 constexpr int kTileMaxW = 64;   // cells per tile along x
 
 // Global-mode exact k-NN over tiles of W consecutive cells of one grid row.

@@ -16,7 +16,11 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--occ", default=os.environ.get("NAVGPU_KNN_OCC", "3"))
 ap.add_argument("--k", type=int, default=8)
 ap.add_argument("--reps", type=int, default=10)
+ap.add_argument("--lib", default=None, help="alternative libnavgpu.so (variant build)")
 a = ap.parse_args()
+if a.lib:
+    import navslam.gpu as _g
+    _g.load_library(a.lib)
 dev = torch.device("cuda", 0)
 g = NavGpu(0, torch.cuda.current_stream(dev).cuda_stream)
 s, t = synth.uniform_pair(512, 2048)
@@ -34,6 +38,6 @@ for _ in range(a.reps):
 torch.cuda.synchronize()
 q_ms, qn = g.timing_read("knn_query")
 b_ms, bn = g.timing_read("knn_build")
-print(json.dumps({"occ": float(a.occ), "k": a.k, "query_us": 1000 * q_ms / qn,
+print(json.dumps({"lib": os.path.basename(a.lib or "libnavgpu.so"), "occ": float(a.occ), "k": a.k, "query_us": 1000 * q_ms / qn,
                   "build_us": 1000 * b_ms / bn, "slow_lanes": slow,
                   "slow_frac": slow / N}))
