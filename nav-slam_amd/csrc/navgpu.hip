@@ -46,6 +46,18 @@ constexpr int kStackDepth = 14;     // implicit-tree height bound, n < 8192
 constexpr int kMaxRowCols = 8191;   // 13-bit stack-entry fields
 constexpr int kCurvTile = 256;
 
+// Diagnostic phase stamps (build with -DNAVGPU_STAMPS; never in the product
+// build): lane 0 of each wave adds s_memtime deltas per phase into g_stamps.
+#ifdef NAVGPU_STAMPS
+__device__ unsigned long long g_stamps[16];
+#define NV_STAMP(v) const unsigned long long v = __builtin_amdgcn_s_memtime()
+#define NV_STAMP_ADD(slot, a, b) \
+  if ((threadIdx.x & 63) == 0) atomicAdd(&g_stamps[slot], (b) - (a))
+#else
+#define NV_STAMP(v)
+#define NV_STAMP_ADD(slot, a, b)
+#endif
+
 // ------------------------------------------------------------------ errors
 char g_err[1024] = "";
 
@@ -968,6 +980,7 @@ __device__ __forceinline__ void knn_one(
     const GridParams &G, const double *__restrict__ tgt, const double qv[3],
     const int c[3], size_t q, Cells cells, Fetch fetch,
     int32_t *__restrict__ oidx, double *__restrict__ odist, const KnnLists &L_) {
+  NV_STAMP(ts0);
   const double qr[3] = {qv[0] - G.o[0], qv[1] - G.o[1], qv[2] - G.o[2]};
   const float qf[3] = {(float)qr[0], (float)qr[1], (float)qr[2]};
   // |f32 difference - exact difference| <= dl: each operand rounded to f32
@@ -1037,6 +1050,8 @@ __device__ __forceinline__ void knn_one(
       }
     }
   }
+  NV_STAMP(ts1);
+  NV_STAMP_ADD(3, ts0, ts1);
   // anything outside the 3x3x3 block is at least L away
   double L = INFINITY;
 #pragma unroll
@@ -1118,6 +1133,9 @@ __device__ __forceinline__ void knn_one(
     L_.slow_q[e] = (int)q;
     L_.slow_thr[e] = dk < INFINITY ? dk2 * (1.0 + 0x1p-46) : INFINITY;
   }
+  NV_STAMP(ts2);
+  NV_STAMP_ADD(4, ts1, ts2);
+  NV_STAMP_ADD(5, 0ull, 1ull);
 }
 
 #ifndef NAVGPU_TILE_THREADS
@@ -1168,6 +1186,7 @@ __global__ __launch_bounds__(kTileThreads) void k_knn(
     step = gridDim.x >> 3;
   }
   for (long long it = first; it < t_hi; it += step) {
+    NV_STAMP(tb0);
     const long long tile = GLOBAL ? (long long)L_.ovf_tiles[it] : it;
     const int row = (int)(tile / tpr), chunk = (int)(tile % tpr);
     const int y = row % G.g[1], z = row / G.g[1];
@@ -1210,6 +1229,9 @@ __global__ __launch_bounds__(kTileThreads) void k_knn(
       }
       __syncthreads();
     }
+    NV_STAMP(tb1);
+    NV_STAMP_ADD(1, tb0, tb1);
+    NV_STAMP_ADD(6, 0ull, 1ull);
     const int cell0 = (z * G.g[1] + y) * G.g[0];
     const int q0 = qstart[cell0 + xa], q1 = qstart[cell0 + xb + 1];
     for (int qi = q0 + threadIdx.x; qi < q1; qi += blockDim.x) {
@@ -1234,6 +1256,8 @@ __global__ __launch_bounds__(kTileThreads) void k_knn(
                    [&](int p) { return rec[p]; }, oidx, odist, L_);
       }
     }
+    NV_STAMP(tb2);
+    NV_STAMP_ADD(2, tb1, tb2);
     __syncthreads();
   }
 }
@@ -1620,6 +1644,20 @@ double navgpu_timing_read(navgpu_ctx *ctx, const char *name, int reset) {
     it->second.clear();
   }
   return ms;
+}
+
+// diagnostic builds only (-DNAVGPU_STAMPS): read and clear the phase stamps
+int navgpu_debug_stamps(unsigned long long *out16) {
+#ifdef NAVGPU_STAMPS
+  HIP_TRY(hipDeviceSynchronize());
+  HIP_TRY(hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_stamps), 16 * 8));
+  unsigned long long z[16] = {0};
+  HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), z, 16 * 8));
+  return NAVGPU_OK;
+#else
+  (void)out16;
+  return NAVGPU_EINVAL;
+#endif
 }
 
 long long navgpu_knn_fallbacks(navgpu_ctx *ctx) {
