@@ -885,16 +885,21 @@ __global__ __launch_bounds__(kScanBlock) void k_scan_apply(
 __global__ __launch_bounds__(256) void k_scatter_targets(
     const double *__restrict__ p, size_t n, const GridParams *__restrict__ gp,
     const int *__restrict__ cellid, const int *__restrict__ slot,
-    const int *__restrict__ start, Rec16 *__restrict__ rec) {
+    const int *__restrict__ start, Rec16 *__restrict__ rec,
+    double *__restrict__ tsort) {
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const GridParams G = *gp;
+  const size_t pos = (size_t)start[cellid[i]] + slot[i];
+  tsort[3 * pos] = p[3 * i];
+  tsort[3 * pos + 1] = p[3 * i + 1];
+  tsort[3 * pos + 2] = p[3 * i + 2];
   Rec16 r;
   r.x = (float)(p[3 * i] - G.o[0]);
   r.y = (float)(p[3 * i + 1] - G.o[1]);
   r.z = (float)(p[3 * i + 2] - G.o[2]);
   r.idx = (int)i;
-  rec[start[cellid[i]] + slot[i]] = r;
+  rec[pos] = r;
 }
 
 __global__ __launch_bounds__(256) void k_scatter_queries(
@@ -977,7 +982,7 @@ struct KnnLists {
 
 template <int K, class Cells, class Fetch>
 __device__ __forceinline__ void knn_one(
-    const GridParams &G, const double *__restrict__ tgt, const double qv[3],
+    const GridParams &G, const double *__restrict__ tsort, const double qv[3],
     const int c[3], size_t q, Cells cells, Fetch fetch,
     int32_t *__restrict__ oidx, double *__restrict__ odist, const KnnLists &L_) {
   NV_STAMP(ts0);
@@ -1013,8 +1018,8 @@ __device__ __forceinline__ void knn_one(
 #pragma unroll 1
   for (int ci = 0; ci < 27; ++ci) {
     const int r = kCellRun[ci], dx = kCellDx[ci];
-    int t0, t1;
-    cells(r, dx, t0, t1);
+    int t0, t1, g0;
+    cells(r, dx, t0, t1, g0);
     if (t0 >= t1) continue;
     if (ci > 0 && key[K] != kNoKey) {
       int dyv, dzv;
@@ -1070,29 +1075,41 @@ __device__ __forceinline__ void knn_one(
     B = fmin(B, V - err);
   }
   bool ok = !overflow && Dq < 1e17;
+  // exact f64 re-evaluation of the K+1 survivors. All loads are issued
+  // unconditionally (an empty slot re-reads slot 0) so their latencies
+  // overlap; coordinates come from the cell-sorted copy (L2-local).
   double ed[KL];
   int ei[KL];
+  if (key[0] != kNoKey) {
+    int gpos[KL];
 #pragma unroll
-  for (int s = 0; s < KL; ++s) {
-    ed[s] = INFINITY;
-    ei[s] = -1;
-    if (key[s] != kNoKey) {
-      const int l = (int)(key[s] & kKeyMask);
-      const int ci = l >> kCellOffBits;
-      int t0, t1;
-      cells(kCellRun[ci], kCellDx[ci], t0, t1);
-      const int id = fetch(t0 + (l & ((1 << kCellOffBits) - 1))).idx;
-      const double *tp = tgt + 3 * (size_t)id;
+    for (int s = 0; s < KL; ++s) {
+      const bool v = key[s] != kNoKey;
+      const int l = (int)((v ? key[s] : key[0]) & kKeyMask);
+      const int ci = l >> kCellOffBits, off = l & ((1 << kCellOffBits) - 1);
+      int t0, t1, g0;
+      cells(kCellRun[ci], kCellDx[ci], t0, t1, g0);
+      ei[s] = v ? fetch(t0 + off).idx : -1;
+      gpos[s] = g0 + off;
+    }
+#pragma unroll
+    for (int s = 0; s < KL; ++s) {
+      const double *tp = tsort + 3 * (size_t)gpos[s];
       const double ddx = tp[0] - qv[0], ddy = tp[1] - qv[1], ddz = tp[2] - qv[2];
       const double dsq = ddx * ddx + ddy * ddy + ddz * ddz;  // utils/kdtree.c:16
-      ed[s] = __builtin_sqrt(dsq);
-      ei[s] = id;
+      ed[s] = ei[s] >= 0 ? __builtin_sqrt(dsq) : INFINITY;
       // an inf/NaN distance is never a neighbour (kdtree.c:117)
-      if (!(ed[s] < INFINITY)) {
+      if (ei[s] >= 0 && !(ed[s] < INFINITY)) {
         ed[s] = INFINITY;
         ei[s] = -1;
         ok = false;
       }
+    }
+  } else {
+#pragma unroll
+    for (int s = 0; s < KL; ++s) {
+      ed[s] = INFINITY;
+      ei[s] = -1;
     }
   }
   // order by (distance, index): the f32 order is almost always already right
@@ -1161,7 +1178,7 @@ constexpr int kTileMaxW = 64;   // cells per tile along x
 template <int K, bool GLOBAL>
 __global__ __launch_bounds__(kTileThreads) void k_knn(
     const GridParams *__restrict__ gp, const int *__restrict__ start,
-    const Rec16 *__restrict__ rec, const double *__restrict__ tgt,
+    const Rec16 *__restrict__ rec, const double *__restrict__ tsort,
     const double *__restrict__ qs, const int *__restrict__ qstart,
     const int *__restrict__ qperm, int32_t *__restrict__ oidx,
     double *__restrict__ odist, KnnLists L_) {
@@ -1240,17 +1257,18 @@ __global__ __launch_bounds__(kTileThreads) void k_knn(
       const int c[3] = {cell_axis(qv[0], G, 0), y, z};
       const int i = c[0] - xa;
       if (!GLOBAL) {
-        knn_one<K>(G, tgt, qv, c, q,
-                   [&](int r, int dx, int &t0, int &t1) {
+        knn_one<K>(G, tsort, qv, c, q,
+                   [&](int r, int dx, int &t0, int &t1, int &g0) {
                      const int sh = sbase[r] - soff[r][0];
-                     t0 = soff[r][i + 1 + dx] + sh;
+                     g0 = soff[r][i + 1 + dx];
+                     t0 = g0 + sh;
                      t1 = soff[r][i + 2 + dx] + sh;
                    },
                    [&](int p) { return srec[p]; }, oidx, odist, L_);
       } else {
-        knn_one<K>(G, tgt, qv, c, q,
-                   [&](int r, int dx, int &t0, int &t1) {
-                     t0 = soff[r][i + 1 + dx];
+        knn_one<K>(G, tsort, qv, c, q,
+                   [&](int r, int dx, int &t0, int &t1, int &g0) {
+                     t0 = g0 = soff[r][i + 1 + dx];
                      t1 = soff[r][i + 2 + dx];
                    },
                    [&](int p) { return rec[p]; }, oidx, odist, L_);
@@ -1290,7 +1308,7 @@ __device__ __forceinline__ void knn_insert(double *kd, int *ki, double d, int id
 template <int K>
 __global__ __launch_bounds__(256) void k_knn_slow(
     const GridParams *__restrict__ gp, const int *__restrict__ start,
-    const Rec16 *__restrict__ rec, const double *__restrict__ tgt,
+    const Rec16 *__restrict__ rec, const double *__restrict__ tsort,
     const double *__restrict__ qs, int32_t *__restrict__ oidx,
     double *__restrict__ odist, KnnLists L_) {
   const GridParams G = *gp;
@@ -1336,7 +1354,7 @@ __global__ __launch_bounds__(256) void k_knn_slow(
           const float fx = rr.x - qf[0], fy = rr.y - qf[1], fz = rr.z - qf[2];
           const float d2f = __builtin_fmaf(fz, fz, __builtin_fmaf(fy, fy, fx * fx));
           if (!(d2f <= thr_f)) continue;
-          const double *tp = tgt + 3 * (size_t)rr.idx;
+          const double *tp = tsort + 3 * (size_t)t;
           const double ddx = tp[0] - qv[0], ddy = tp[1] - qv[1], ddz = tp[2] - qv[2];
           const double dsq = ddx * ddx + ddy * ddy + ddz * ddz;
           if (!(dsq <= thr)) continue;
@@ -1422,7 +1440,7 @@ namespace {
 enum Slot {
   kBBox = 1, kParams, kCnt, kStart, kBSum, kCellId, kSlotBuf, kRec, kTan,
   kKdFc, kKdP, kKdT, kQStart, kQCell, kQSlot, kQPerm, kStats, kOvf, kSlowQ,
-  kSlowThr,
+  kSlowThr, kTSort,
   kH0 = 100, kH1, kH2, kH3, kH4, kH5,
 };
 
@@ -1975,6 +1993,7 @@ int navgpu_knn_dev(navgpu_ctx *ctx, const double *tgt, size_t nt,
   int *tcnt, *tstart, *qcnt, *qstart, *bsum, *tcell = nullptr, *tslot = nullptr;
   int *qcell, *qslot, *qperm;
   Rec16 *rec = nullptr;
+  double *tsort = nullptr;
   RC(ws(ctx, kBBox, (size_t)kBBoxBlocks * 6, &part));
   RC(ws(ctx, kParams, 1, &gp));
   RC(ws(ctx, kCnt, 2 * (size_t)nscan, &tcnt));
@@ -1986,6 +2005,7 @@ int navgpu_knn_dev(navgpu_ctx *ctx, const double *tgt, size_t nt,
     RC(ws(ctx, kCellId, nt, &tcell));
     RC(ws(ctx, kSlotBuf, nt, &tslot));
     RC(ws(ctx, kRec, nt, &rec));
+    RC(ws(ctx, kTSort, 3 * nt, &tsort));
   }
   RC(ws(ctx, kQCell, nq, &qcell));
   RC(ws(ctx, kQSlot, nq, &qslot));
@@ -2022,7 +2042,7 @@ int navgpu_knn_dev(navgpu_ctx *ctx, const double *tgt, size_t nt,
     }
     if (nt) {
       hipLaunchKernelGGL(k_scatter_targets, dim3(grid1d(nt, 256)), dim3(256), 0, s, tgt,
-                         nt, gp, tcell, tslot, tstart, rec);
+                         nt, gp, tcell, tslot, tstart, rec, tsort);
       CHECK_LAUNCH("k_scatter_targets");
     }
     hipLaunchKernelGGL(k_scatter_queries, dim3(grid1d(nq, 256)), dim3(256), 0, s, nq,
@@ -2045,12 +2065,12 @@ int navgpu_knn_dev(navgpu_ctx *ctx, const double *tgt, size_t nt,
   const dim3 gs(std::max<unsigned>(1, std::min<unsigned>(2048, grid1d(nq, 256))));
 #define KNN_CASE(KK)                                                              \
   case KK:                                                                        \
-    hipLaunchKernelGGL((k_knn<KK, false>), g, b, 0, s, gp, tstart, rec, tgt,     \
+    hipLaunchKernelGGL((k_knn<KK, false>), g, b, 0, s, gp, tstart, rec, tsort,   \
                        queries, qstart, qperm, idx, dist, lists);                 \
-    hipLaunchKernelGGL((k_knn<KK, true>), g, b, 0, s, gp, tstart, rec, tgt,      \
+    hipLaunchKernelGGL((k_knn<KK, true>), g, b, 0, s, gp, tstart, rec, tsort,    \
                        queries, qstart, qperm, idx, dist, lists);                 \
     hipLaunchKernelGGL((k_knn_slow<KK>), gs, dim3(256), 0, s, gp, tstart, rec,    \
-                       tgt, queries, idx, dist, lists);                           \
+                       tsort, queries, idx, dist, lists);                         \
     break;
   switch (k) {
     KNN_CASE(1)
