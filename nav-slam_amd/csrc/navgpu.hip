@@ -1015,45 +1015,58 @@ __device__ __forceinline__ void knn_one(
 #pragma unroll
   for (int s = 0; s < KL; ++s) key[s] = kNoKey;
   bool overflow = false;  // a cell with more than 2^kCellOffBits candidates
+  typedef float f2 __attribute__((ext_vector_type(2)));
+  const f2 qx2 = {qf[0], qf[0]}, qy2 = {qf[1], qf[1]}, qz2 = {qf[2], qf[2]};
+  // software pipeline: the pair being processed (a) was read one step ahead;
+  // the next pair of this cell and the first pair of the next cell are read
+  // before (a) is consumed, so LDS latency hides behind the arithmetic
+  int t0, t1, g0;
+  cells(kCellRun[0], kCellDx[0], t0, t1, g0);
+  Rec16 a0 = fetch(t0), a1 = fetch(t0 + 1);
 #pragma unroll 1
   for (int ci = 0; ci < 27; ++ci) {
     const int r = kCellRun[ci], dx = kCellDx[ci];
-    int t0, t1, g0;
-    cells(r, dx, t0, t1, g0);
-    if (t0 >= t1) continue;
-    if (ci > 0 && key[K] != kNoKey) {
+    int n0 = 0, n1 = 0, ng0 = 0;
+    if (ci < 26) cells(kCellRun[ci + 1], kCellDx[ci + 1], n0, n1, ng0);
+    const Rec16 b0 = fetch(n0), b1 = fetch(n0 + 1);
+    bool visit = t0 < t1;
+    if (visit && ci > 0 && key[K] != kNoKey) {
       int dyv, dzv;
       run_dydz(r, dyv, dzv);
       const float bx = dx < 0 ? e2v[0][0] : (dx > 0 ? e2v[0][2] : e2v[0][1]);
       const float by = dyv < 0 ? e2v[1][0] : (dyv > 0 ? e2v[1][2] : e2v[1][1]);
       const float bz = dzv < 0 ? e2v[2][0] : (dzv > 0 ? e2v[2][2] : e2v[2][1]);
       const float bd2 = (bx + by) + bz;
-      if (bd2 * (1.0f - 0x1p-20f) > __uint_as_float(key[K] & ~kKeyMask)) continue;
+      visit = !(bd2 * (1.0f - 0x1p-20f) > __uint_as_float(key[K] & ~kKeyMask));
     }
-    overflow |= (t1 - t0) > (1 << kCellOffBits);
-    const uint32_t cid = (uint32_t)ci << kCellOffBits;
-    for (int t = t0; t < t1; t += 2) {
-      Rec16 rp[2];
-      rp[0] = fetch(t);
-      rp[1] = fetch(t + 1 < t1 ? t + 1 : t);
-      // the pair's f32 distances in packed math (v_pk_*_f32)
-      typedef float f2 __attribute__((ext_vector_type(2)));
-      const f2 px = {rp[0].x, rp[1].x}, py = {rp[0].y, rp[1].y}, pz = {rp[0].z, rp[1].z};
-      const f2 qx2 = {qf[0], qf[0]}, qy2 = {qf[1], qf[1]}, qz2 = {qf[2], qf[2]};
-      const f2 fx2 = px - qx2, fy2 = py - qy2, fz2 = pz - qz2;
-      const f2 d22 = __builtin_elementwise_fma(
-          fz2, fz2, __builtin_elementwise_fma(fy2, fy2, fx2 * fx2));
+    if (visit) {
+      overflow |= (t1 - t0) > (1 << kCellOffBits);
+      const uint32_t cid = (uint32_t)ci << kCellOffBits;
+      for (int t = t0; t < t1; t += 2) {
+        const Rec16 c0 = fetch(t + 2), c1 = fetch(t + 3);  // next pair
+        const f2 px = {a0.x, a1.x}, py = {a0.y, a1.y}, pz = {a0.z, a1.z};
+        const f2 fx2 = px - qx2, fy2 = py - qy2, fz2 = pz - qz2;  // packed f32
+        const f2 d22 = __builtin_elementwise_fma(
+            fz2, fz2, __builtin_elementwise_fma(fy2, fy2, fx2 * fx2));
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const float d2 = d22[j];
-        uint32_t kk = (__float_as_uint(d2) & ~kKeyMask) | cid |
-                      ((uint32_t)(t + j - t0) & ((1u << kCellOffBits) - 1));
-        if (j && t + 1 >= t1) kk = kNoKey;  // padding past the cell end
+        for (int j = 0; j < 2; ++j) {
+          const float d2 = d22[j];
+          uint32_t kk = (__float_as_uint(d2) & ~kKeyMask) | cid |
+                        ((uint32_t)(t + j - t0) & ((1u << kCellOffBits) - 1));
+          if (j && t + 1 >= t1) kk = kNoKey;  // padding past the cell end
 #pragma unroll
-        for (int s = K; s > 0; --s) key[s] = umed3(key[s - 1], key[s], kk);
-        key[0] = min(key[0], kk);
+          for (int s = K; s > 0; --s) key[s] = umed3(key[s - 1], key[s], kk);
+          key[0] = min(key[0], kk);
+        }
+        a0 = c0;
+        a1 = c1;
       }
     }
+    a0 = b0;
+    a1 = b1;
+    t0 = n0;
+    t1 = n1;
+    g0 = ng0;
   }
   NV_STAMP(ts1);
   NV_STAMP_ADD(3, ts0, ts1);
@@ -1251,6 +1264,7 @@ __global__ __launch_bounds__(kTileThreads) void k_knn(
     NV_STAMP_ADD(6, 0ull, 1ull);
     const int cell0 = (z * G.g[1] + y) * G.g[0];
     const int q0 = qstart[cell0 + xa], q1 = qstart[cell0 + xb + 1];
+    const int ntm1 = max(start[G.ncells] - 1, 0);  // last valid record (prefetch clamp)
     for (int qi = q0 + threadIdx.x; qi < q1; qi += blockDim.x) {
       const size_t q = (size_t)qperm[qi];
       const double qv[3] = {qs[3 * q], qs[3 * q + 1], qs[3 * q + 2]};
@@ -1264,14 +1278,14 @@ __global__ __launch_bounds__(kTileThreads) void k_knn(
                      t0 = g0 + sh;
                      t1 = soff[r][i + 2 + dx] + sh;
                    },
-                   [&](int p) { return srec[p]; }, oidx, odist, L_);
+                   [&](int p) { return srec[min(p, kTileRec - 1)]; }, oidx, odist, L_);
       } else {
         knn_one<K>(G, tsort, qv, c, q,
                    [&](int r, int dx, int &t0, int &t1, int &g0) {
                      t0 = g0 = soff[r][i + 1 + dx];
                      t1 = soff[r][i + 2 + dx];
                    },
-                   [&](int p) { return rec[p]; }, oidx, odist, L_);
+                   [&](int p) { return rec[min(p, ntm1)]; }, oidx, odist, L_);
       }
     }
     NV_STAMP(tb2);
