@@ -1189,7 +1189,10 @@ constexpr int kTileMaxW = 64;   // cells per tile along x
 // is appended to the overflow list. GLOBAL = true: the overflow tiles, read
 // straight from the global record array.
 template <int K, bool GLOBAL>
-__global__ __launch_bounds__(kTileThreads) void k_knn(
+#ifndef NAVGPU_KNN_MINW
+#define NAVGPU_KNN_MINW 1
+#endif
+__global__ __launch_bounds__(kTileThreads, NAVGPU_KNN_MINW) void k_knn(
     const GridParams *__restrict__ gp, const int *__restrict__ start,
     const Rec16 *__restrict__ rec, const double *__restrict__ tsort,
     const double *__restrict__ qs, const int *__restrict__ qstart,
