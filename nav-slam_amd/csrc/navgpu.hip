@@ -1030,7 +1030,11 @@ __device__ __forceinline__ void knn_one(
     if (ci < 26) cells(kCellRun[ci + 1], kCellDx[ci + 1], n0, n1, ng0);
     const Rec16 b0 = fetch(n0), b1 = fetch(n0 + 1);
     bool visit = t0 < t1;
+#ifdef NAVGPU_DBG_NOCULL
+    if (false) {
+#else
     if (visit && ci > 0 && key[K] != kNoKey) {
+#endif
       int dyv, dzv;
       run_dydz(r, dyv, dzv);
       const float bx = dx < 0 ? e2v[0][0] : (dx > 0 ? e2v[0][2] : e2v[0][1]);
@@ -1054,8 +1058,10 @@ __device__ __forceinline__ void knn_one(
           uint32_t kk = (__float_as_uint(d2) & ~kKeyMask) | cid |
                         ((uint32_t)(t + j - t0) & ((1u << kCellOffBits) - 1));
           if (j && t + 1 >= t1) kk = kNoKey;  // padding past the cell end
+#ifndef NAVGPU_DBG_NOINSERT
 #pragma unroll
           for (int s = K; s > 0; --s) key[s] = umed3(key[s - 1], key[s], kk);
+#endif
           key[0] = min(key[0], kk);
         }
         a0 = c0;
@@ -1093,7 +1099,11 @@ __device__ __forceinline__ void knn_one(
   // overlap; coordinates come from the cell-sorted copy (L2-local).
   double ed[KL];
   int ei[KL];
+#ifdef NAVGPU_DBG_NOEXACT
+  if (false) {
+#else
   if (key[0] != kNoKey) {
+#endif
     int gpos[KL];
 #pragma unroll
     for (int s = 0; s < KL; ++s) {

@@ -1,6 +1,6 @@
 #!/bin/bash
-# Build experimental libnavgpu variants (compile-time tile knobs) into
-# nav-slam_amd/lib/variants/ for side-by-side timing with knn_probe.py --lib.
+# Build experimental libnavgpu variants (compile-time knobs / timing-only
+# ablations) into nav-slam_amd/lib/variants/ for knn_probe.py --lib.
 cd "$(dirname "$0")/.." || exit 1
 rm -rf nav-slam_amd/lib/variants; mkdir -p nav-slam_amd/lib/variants
 build() {  # build <name> <defines...>
@@ -9,10 +9,10 @@ build() {  # build <name> <defines...>
     -Iinclude "$@" -shared -o "nav-slam_amd/lib/variants/libnavgpu_$name.so" \
     nav-slam_amd/csrc/navgpu.hip &
 }
-build base -DNAVGPU_TILE_THREADS=256 -DNAVGPU_TILE_REC=2048
-build r1024_w5 -DNAVGPU_TILE_THREADS=256 -DNAVGPU_TILE_REC=1024 -DNAVGPU_TILE_QUERIES=110.0 -DNAVGPU_KNN_MINW=5
-build r1024_w6 -DNAVGPU_TILE_THREADS=256 -DNAVGPU_TILE_REC=1024 -DNAVGPU_TILE_QUERIES=110.0 -DNAVGPU_KNN_MINW=6
-build r768_w8 -DNAVGPU_TILE_THREADS=256 -DNAVGPU_TILE_REC=768 -DNAVGPU_TILE_QUERIES=80.0 -DNAVGPU_KNN_MINW=8
-build t128_r1024_w6 -DNAVGPU_TILE_THREADS=128 -DNAVGPU_TILE_REC=1024 -DNAVGPU_TILE_QUERIES=110.0 -DNAVGPU_KNN_MINW=6
+build base
+build noinsert -DNAVGPU_DBG_NOINSERT
+build noexact -DNAVGPU_DBG_NOEXACT
+build nocull -DNAVGPU_DBG_NOCULL
+build noins_noex -DNAVGPU_DBG_NOINSERT -DNAVGPU_DBG_NOEXACT
 wait
 ls nav-slam_amd/lib/variants
