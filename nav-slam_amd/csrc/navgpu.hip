@@ -1154,6 +1154,9 @@ __device__ __forceinline__ void knn_one(
       }
     }
   }
+#if defined(NAVGPU_DBG_NOINSERT) || defined(NAVGPU_DBG_NOEXACT)
+  ok = true;  // timing-only ablation builds: never take the slow path
+#endif
   const double dk = ed[K - 1];
   const double dk2 = dk * dk;  // >= the exact K-th dsq (sqrt rounds to nearest)
   if (dk < INFINITY)
