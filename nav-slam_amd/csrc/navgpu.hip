@@ -1154,15 +1154,15 @@ __device__ __forceinline__ void knn_one(
       }
     }
   }
-#if defined(NAVGPU_DBG_NOINSERT) || defined(NAVGPU_DBG_NOEXACT)
-  ok = true;  // timing-only ablation builds: never take the slow path
-#endif
   const double dk = ed[K - 1];
   const double dk2 = dk * dk;  // >= the exact K-th dsq (sqrt rounds to nearest)
   if (dk < INFINITY)
     ok = ok && B > dk2 * (1.0 + 0x1p-46);
   else
     ok = ok && B == INFINITY;  // fewer than K neighbours: only if all was seen
+#if defined(NAVGPU_DBG_NOINSERT) || defined(NAVGPU_DBG_NOEXACT)
+  ok = true;  // timing-only ablation builds: never take the slow path
+#endif
   if (ok) {
 #pragma unroll
     for (int s = 0; s < K; ++s) {
