@@ -691,7 +691,7 @@ struct __align__(16) Rec16 {  // cell-sorted target: (coords - origin) in f32
 };
 
 constexpr int kBBoxBlocks = 1024;
-constexpr int kKeyBits = 10;  // local id in the low bits of a key: cell (5) | offset (5)
+constexpr int kKeyBits = 10;  // local id in the low bits of a key: run (4) | offset (6)
 constexpr uint32_t kKeyMask = (1u << kKeyBits) - 1;
 constexpr uint32_t kNoKey = 0xffffffffu;
 
@@ -954,25 +954,21 @@ __device__ __forceinline__ void run_dydz(int r, int &dy, int &dz) {
 }
 
 // One query of the global-mode k-NN.
-// Fast path over the query's 3x3x3 cell neighbourhood, own cell first, then
-// faces, edges, corners; a cell whose box is already beyond the current
-// (K+1)-th candidate is skipped. Each candidate gets an f32 distance
-// (coordinates relative to the grid origin) packed with its local id
-// (cell slot | offset) into a 32-bit key; a sorted list of the K+1 smallest
-// keys is kept by branch-free median-of-3 insertion. The K+1 survivors are
-// then re-evaluated with the reference f64 formula and ordered by
-// (distance, index); the result is certified exact when every candidate left
-// out (visited but not kept, skipped, or outside the block) is provably
-// farther than the K-th, using the f32 error bound. Otherwise (near ties, a
-// neighbourhood reaching past the block, overfull cells) the query is queued
-// for k_knn_slow with the K-th distance found as its starting bound.
-// cells(r, dx, t0, t1): record range of cell x+dx in run r, in the index space
-// of fetch (LDS tile or global array).
-__constant__ signed char kCellRun[27] = {0, 0, 0, 1, 2, 3, 4, 1, 1, 2, 2, 3, 3, 4,
-                                         4, 5, 6, 7, 8, 5, 5, 6, 6, 7, 7, 8, 8};
-__constant__ signed char kCellDx[27] = {0, -1, 1, 0, 0, 0, 0, -1, 1, -1, 1, -1, 1, -1,
-                                        1, 0, 0, 0, 0, -1, 1, -1, 1, -1, 1, -1, 1};
-constexpr int kCellOffBits = 5;  // candidates per cell slot in a key
+// Fast path over the query's 3x3x3 cell neighbourhood, taken as 9 runs: the
+// three cells x-1..x+1 of one (y, z) row are contiguous in the cell-sorted
+// arrays, so each run is one record range (own row first, then faces, then
+// corners). Each candidate gets an f32 distance (coordinates relative to the
+// grid origin) packed with its local id (run | offset) into a 32-bit key; a
+// sorted list of the K+1 smallest keys is kept by branch-free median-of-3
+// insertion. The K+1 survivors are then re-evaluated with the reference f64
+// formula and ordered by (distance, index); the result is certified exact when
+// every candidate left out (visited but not kept, or outside the block) is
+// provably farther than the K-th, using the f32 error bound. Otherwise (near
+// ties, a neighbourhood reaching past the block, overfull runs) the query is
+// queued for k_knn_slow with the K-th distance found as its starting bound.
+// runs(r, t0, t1, g0): record range [t0, t1) of run r in the index space of
+// fetch (LDS tile or global array) and g0 = its first record's global position.
+constexpr int kRunOffBits = 6;  // candidates per run addressable by a key
 
 struct KnnLists {
   int *ovf_tiles, *n_ovf;  // tiles whose segments overflow the LDS budget
@@ -980,10 +976,10 @@ struct KnnLists {
   double *slow_thr;        // their starting bound (K-th dsq upper bound)
 };
 
-template <int K, class Cells, class Fetch>
+template <int K, class Runs, class Fetch>
 __device__ __forceinline__ void knn_one(
     const GridParams &G, const double *__restrict__ tsort, const double qv[3],
-    const int c[3], size_t q, Cells cells, Fetch fetch,
+    const int c[3], size_t q, Runs runs, Fetch fetch,
     int32_t *__restrict__ oidx, double *__restrict__ odist, const KnnLists &L_) {
   NV_STAMP(ts0);
   const double qr[3] = {qv[0] - G.o[0], qv[1] - G.o[1], qv[2] - G.o[2]};
@@ -993,86 +989,43 @@ __device__ __forceinline__ void knn_one(
   const double Dq = fmax(G.emax + G.h,
                          fmax(fabs(qr[0]), fmax(fabs(qr[1]), fabs(qr[2]))));
   const double dl = Dq * 0x1p-22;
-  // per-axis lower bounds on the distance to the cells at offsets -1, 0, +1
-  // (shrunk by the f32 slack), squared: a cell's box bound is a sum of three
-  float e2v[3][3];
-#pragma unroll
-  for (int a = 0; a < 3; ++a) {
-    const double lo = c[a] * G.h, hi = (c[a] + 1) * G.h;
-    const double m = 2.0 * dl + 2.0 * G.delta;
-    const double dm = fmax(0.0, qr[a] - lo - m);
-    const double dp = fmax(0.0, hi - qr[a] - m);
-    const double d0 = fmax(0.0, fmax(c[a] > 0 ? lo - qr[a] : 0.0,
-                                     c[a] < G.g[a] - 1 ? qr[a] - hi : 0.0) - m);
-    const float fm = (float)dm * (1.0f - 0x1p-20f), f0 = (float)d0 * (1.0f - 0x1p-20f),
-                fp = (float)dp * (1.0f - 0x1p-20f);
-    e2v[a][0] = fm * fm;
-    e2v[a][1] = f0 * f0;
-    e2v[a][2] = fp * fp;
-  }
   constexpr int KL = K + 1;
   uint32_t key[KL];
 #pragma unroll
   for (int s = 0; s < KL; ++s) key[s] = kNoKey;
-  bool overflow = false;  // a cell with more than 2^kCellOffBits candidates
+  bool overflow = false;  // a run with more than 2^kRunOffBits candidates
   typedef float f2 __attribute__((ext_vector_type(2)));
   const f2 qx2 = {qf[0], qf[0]}, qy2 = {qf[1], qf[1]}, qz2 = {qf[2], qf[2]};
-  // software pipeline: the pair being processed (a) was read one step ahead;
-  // the next pair of this cell and the first pair of the next cell are read
-  // before (a) is consumed, so LDS latency hides behind the arithmetic
-  int t0, t1, g0;
-  cells(kCellRun[0], kCellDx[0], t0, t1, g0);
-  Rec16 a0 = fetch(t0), a1 = fetch(t0 + 1);
 #pragma unroll 1
-  for (int ci = 0; ci < 27; ++ci) {
-    const int r = kCellRun[ci], dx = kCellDx[ci];
-    int n0 = 0, n1 = 0, ng0 = 0;
-    if (ci < 26) cells(kCellRun[ci + 1], kCellDx[ci + 1], n0, n1, ng0);
-    const Rec16 b0 = fetch(n0), b1 = fetch(n0 + 1);
-    bool visit = t0 < t1;
-#ifdef NAVGPU_DBG_NOCULL
-    if (false) {
-#else
-    if (visit && ci > 0 && key[K] != kNoKey) {
-#endif
-      int dyv, dzv;
-      run_dydz(r, dyv, dzv);
-      const float bx = dx < 0 ? e2v[0][0] : (dx > 0 ? e2v[0][2] : e2v[0][1]);
-      const float by = dyv < 0 ? e2v[1][0] : (dyv > 0 ? e2v[1][2] : e2v[1][1]);
-      const float bz = dzv < 0 ? e2v[2][0] : (dzv > 0 ? e2v[2][2] : e2v[2][1]);
-      const float bd2 = (bx + by) + bz;
-      visit = !(bd2 * (1.0f - 0x1p-20f) > __uint_as_float(key[K] & ~kKeyMask));
-    }
-    if (visit) {
-      overflow |= (t1 - t0) > (1 << kCellOffBits);
-      const uint32_t cid = (uint32_t)ci << kCellOffBits;
-      for (int t = t0; t < t1; t += 2) {
-        const Rec16 c0 = fetch(t + 2), c1 = fetch(t + 3);  // next pair
-        const f2 px = {a0.x, a1.x}, py = {a0.y, a1.y}, pz = {a0.z, a1.z};
-        const f2 fx2 = px - qx2, fy2 = py - qy2, fz2 = pz - qz2;  // packed f32
-        const f2 d22 = __builtin_elementwise_fma(
-            fz2, fz2, __builtin_elementwise_fma(fy2, fy2, fx2 * fx2));
+  for (int r = 0; r < 9; ++r) {
+    int t0, t1, g0;
+    runs(r, t0, t1, g0);
+    overflow |= (t1 - t0) > (1 << kRunOffBits);
+    const uint32_t rid = (uint32_t)r << kRunOffBits;
+    // the pair being processed was read one step ahead (LDS latency hides
+    // behind the arithmetic of the previous pair)
+    Rec16 a0 = fetch(t0), a1 = fetch(t0 + 1);
+    for (int t = t0; t < t1; t += 2) {
+      const Rec16 c0 = fetch(t + 2), c1 = fetch(t + 3);  // next pair
+      const f2 px = {a0.x, a1.x}, py = {a0.y, a1.y}, pz = {a0.z, a1.z};
+      const f2 fx2 = px - qx2, fy2 = py - qy2, fz2 = pz - qz2;  // packed f32
+      const f2 d22 = __builtin_elementwise_fma(
+          fz2, fz2, __builtin_elementwise_fma(fy2, fy2, fx2 * fx2));
 #pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          const float d2 = d22[j];
-          uint32_t kk = (__float_as_uint(d2) & ~kKeyMask) | cid |
-                        ((uint32_t)(t + j - t0) & ((1u << kCellOffBits) - 1));
-          if (j && t + 1 >= t1) kk = kNoKey;  // padding past the cell end
+      for (int j = 0; j < 2; ++j) {
+        const float d2 = d22[j];
+        uint32_t kk = (__float_as_uint(d2) & ~kKeyMask) | rid |
+                      ((uint32_t)(t + j - t0) & ((1u << kRunOffBits) - 1));
+        if (j && t + 1 >= t1) kk = kNoKey;  // padding past the run end
 #ifndef NAVGPU_DBG_NOINSERT
 #pragma unroll
-          for (int s = K; s > 0; --s) key[s] = umed3(key[s - 1], key[s], kk);
+        for (int s = K; s > 0; --s) key[s] = umed3(key[s - 1], key[s], kk);
 #endif
-          key[0] = min(key[0], kk);
-        }
-        a0 = c0;
-        a1 = c1;
+        key[0] = min(key[0], kk);
       }
+      a0 = c0;
+      a1 = c1;
     }
-    a0 = b0;
-    a1 = b1;
-    t0 = n0;
-    t1 = n1;
-    g0 = ng0;
   }
   NV_STAMP(ts1);
   NV_STAMP_ADD(3, ts0, ts1);
@@ -1109,9 +1062,9 @@ __device__ __forceinline__ void knn_one(
     for (int s = 0; s < KL; ++s) {
       const bool v = key[s] != kNoKey;
       const int l = (int)((v ? key[s] : key[0]) & kKeyMask);
-      const int ci = l >> kCellOffBits, off = l & ((1 << kCellOffBits) - 1);
+      const int r = l >> kRunOffBits, off = l & ((1 << kRunOffBits) - 1);
       int t0, t1, g0;
-      cells(kCellRun[ci], kCellDx[ci], t0, t1, g0);
+      runs(r, t0, t1, g0);
       ei[s] = v ? fetch(t0 + off).idx : -1;
       gpos[s] = g0 + off;
     }
@@ -1288,18 +1241,18 @@ __global__ __launch_bounds__(kTileThreads, NAVGPU_KNN_MINW) void k_knn(
       const int i = c[0] - xa;
       if (!GLOBAL) {
         knn_one<K>(G, tsort, qv, c, q,
-                   [&](int r, int dx, int &t0, int &t1, int &g0) {
+                   [&](int r, int &t0, int &t1, int &g0) {
                      const int sh = sbase[r] - soff[r][0];
-                     g0 = soff[r][i + 1 + dx];
+                     g0 = soff[r][i];
                      t0 = g0 + sh;
-                     t1 = soff[r][i + 2 + dx] + sh;
+                     t1 = soff[r][i + 3] + sh;
                    },
                    [&](int p) { return srec[min(p, kTileRec - 1)]; }, oidx, odist, L_);
       } else {
         knn_one<K>(G, tsort, qv, c, q,
-                   [&](int r, int dx, int &t0, int &t1, int &g0) {
-                     t0 = g0 = soff[r][i + 1 + dx];
-                     t1 = soff[r][i + 2 + dx];
+                   [&](int r, int &t0, int &t1, int &g0) {
+                     t0 = g0 = soff[r][i];
+                     t1 = soff[r][i + 3];
                    },
                    [&](int p) { return rec[min(p, ntm1)]; }, oidx, odist, L_);
       }
