@@ -735,17 +735,24 @@ __global__ __launch_bounds__(256) void k_grid_params(const double *__restrict__ 
                                                      int nparts, size_t n, int cap,
                                                      double occ, size_t nq,
                                                      GridParams *gp) {
-  __shared__ double s[256][6];
+  __shared__ double s[4][6];
   double v6[6] = {INFINITY, INFINITY, INFINITY, -INFINITY, -INFINITY, -INFINITY};
   for (int b = threadIdx.x; b < nparts; b += blockDim.x)
     for (int a = 0; a < 6; ++a)
       v6[a] = a < 3 ? fmin(v6[a], part[b * 6 + a]) : fmax(v6[a], part[b * 6 + a]);
-  for (int a = 0; a < 6; ++a) s[threadIdx.x][a] = v6[a];
+#pragma unroll
+  for (int a = 0; a < 3; ++a)
+    for (int o = kWave / 2; o > 0; o >>= 1) {
+      v6[a] = fmin(v6[a], __shfl_xor(v6[a], o, kWave));
+      v6[3 + a] = fmax(v6[3 + a], __shfl_xor(v6[3 + a], o, kWave));
+    }
+  if ((threadIdx.x & (kWave - 1)) == 0)
+    for (int a = 0; a < 6; ++a) s[threadIdx.x / kWave][a] = v6[a];
   __syncthreads();
   if (threadIdx.x != 0) return;
-  for (int t = 1; t < (int)blockDim.x; ++t)
+  for (int w = 1; w < (int)blockDim.x / kWave; ++w)
     for (int a = 0; a < 6; ++a)
-      v6[a] = a < 3 ? fmin(v6[a], s[t][a]) : fmax(v6[a], s[t][a]);
+      v6[a] = a < 3 ? fmin(v6[a], s[w][a]) : fmax(v6[a], s[w][a]);
   GridParams G;
   double lo[3], ext[3];
   bool any = n > 0;
@@ -814,17 +821,6 @@ __device__ __forceinline__ int cell_of(const double *p, const GridParams &G) {
          cell_axis(p[0], G, 0);
 }
 
-__global__ __launch_bounds__(256) void k_cell_count(
-    const double *__restrict__ p, size_t n, const GridParams *__restrict__ gp,
-    int *__restrict__ cnt, int *__restrict__ cellid, int *__restrict__ slot) {
-  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const GridParams G = *gp;
-  const int c = cell_of(p + 3 * i, G);
-  cellid[i] = c;
-  slot[i] = atomicAdd(&cnt[c], 1);
-}
-
 constexpr int kScanBlock = 1024, kScanPer = 4,
               kScanTile = kScanBlock * kScanPer;
 
@@ -882,32 +878,154 @@ __global__ __launch_bounds__(kScanBlock) void k_scan_apply(
   }
 }
 
-__global__ __launch_bounds__(256) void k_scatter_targets(
-    const double *__restrict__ p, size_t n, const GridParams *__restrict__ gp,
-    const int *__restrict__ cellid, const int *__restrict__ slot,
-    const int *__restrict__ start, Rec16 *__restrict__ rec,
-    double *__restrict__ tsort) {
-  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const GridParams G = *gp;
-  const size_t pos = (size_t)start[cellid[i]] + slot[i];
-  tsort[3 * pos] = p[3 * i];
-  tsort[3 * pos + 1] = p[3 * i + 1];
-  tsort[3 * pos + 2] = p[3 * i + 2];
-  Rec16 r;
-  r.x = (float)(p[3 * i] - G.o[0]);
-  r.y = (float)(p[3 * i + 1] - G.o[1]);
-  r.z = (float)(p[3 * i + 2] - G.o[2]);
-  r.idx = (int)i;
-  rec[pos] = r;
+// ---- cell binning: counting sort of both clouds by grid cell --------------
+// Scattered global atomics run at the memory side on this part (~24 G/s
+// whatever their scope), so the sort uses none: LDS histograms and LDS ranks
+// only.
+//  k_bin_hist    each block takes a contiguous chunk of points and counts
+//                their coarse bucket (cell >> shift) in LDS; counts land in a
+//                bucket-major table[b * nblk + block], so ONE exclusive scan
+//                of the table gives every (bucket, block) its output offset.
+//  k_bin_scatter same chunks: each point gets an LDS rank within its
+//                (bucket, block) and moves to the coarse-bucketed array.
+//  k_bin_fine    one block per bucket: LDS counting sort over the bucket's
+//                2^shift cells, writes start[] for them and every point at its
+//                final cell-sorted position (target: Rec16 + f64 copy;
+//                query: its index). Order inside a cell is unspecified: the
+//                k-NN result does not depend on it (ties are resolved by
+//                (distance, index) in the exact stage).
+// Side 0 = targets, side 1 = queries; both are handled by the same launches
+// (block ranges), and their tables are concatenated so one scan covers both.
+struct BinPt {
+  double x, y, z;
+  int idx, cell;
+};
+struct BinSide {
+  const double *p;
+  int n, P, nblk;
+  int tab;  // offset of this side's table in the concatenated table
+  int sub;  // subtracted from scanned offsets (targets' total, for side 1)
+  int *start;
+};
+struct BinJob {
+  BinSide s[2];
+  int shift, nb;  // buckets per side
+  BinPt *bin_t;
+  int2 *bin_q;    // (idx, cell)
+  Rec16 *rec;
+  double *tsort;
+  int *qperm;
+};
+constexpr int kBinMaxBuckets = 4096;
+constexpr int kBinMaxShift = 15;
+
+__device__ __forceinline__ int bin_side(const BinJob &J, int &blk) {
+  const int side = blk >= J.s[0].nblk ? 1 : 0;
+  if (side) blk -= J.s[0].nblk;
+  return side;
 }
 
-__global__ __launch_bounds__(256) void k_scatter_queries(
-    size_t n, const int *__restrict__ cellid, const int *__restrict__ slot,
-    const int *__restrict__ start, int *__restrict__ perm) {
-  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  perm[start[cellid[i]] + slot[i]] = (int)i;
+__global__ __launch_bounds__(256) void k_bin_hist(BinJob J,
+                                                  const GridParams *__restrict__ gp,
+                                                  int *__restrict__ table) {
+  __shared__ int hist[kBinMaxBuckets];
+  int blk = blockIdx.x;
+  const BinSide S = J.s[bin_side(J, blk)];
+  const GridParams G = *gp;
+  for (int b = threadIdx.x; b < J.nb; b += blockDim.x) hist[b] = 0;
+  __syncthreads();
+  const int i1 = min(S.n, (blk + 1) * S.P);
+  for (int i = blk * S.P + threadIdx.x; i < i1; i += blockDim.x)
+    atomicAdd(&hist[cell_of(S.p + 3 * (size_t)i, G) >> J.shift], 1);
+  __syncthreads();
+  for (int b = threadIdx.x; b < J.nb; b += blockDim.x)
+    table[S.tab + b * S.nblk + blk] = hist[b];
+  if (blk == 0 && threadIdx.x == 0) table[S.tab + J.nb * S.nblk] = 0;  // sentinel
+}
+
+__global__ __launch_bounds__(256) void k_bin_scatter(BinJob J,
+                                                     const GridParams *__restrict__ gp,
+                                                     const int *__restrict__ offs) {
+  __shared__ int cur[kBinMaxBuckets];
+  int blk = blockIdx.x;
+  const int side = bin_side(J, blk);
+  const BinSide S = J.s[side];
+  const GridParams G = *gp;
+  for (int b = threadIdx.x; b < J.nb; b += blockDim.x)
+    cur[b] = offs[S.tab + b * S.nblk + blk] - S.sub;
+  __syncthreads();
+  const int i1 = min(S.n, (blk + 1) * S.P);
+  for (int i = blk * S.P + threadIdx.x; i < i1; i += blockDim.x) {
+    const double *pp = S.p + 3 * (size_t)i;
+    const int c = cell_of(pp, G);
+    const int pos = atomicAdd(&cur[c >> J.shift], 1);
+    if (side == 0) {
+      BinPt t;
+      t.x = pp[0];
+      t.y = pp[1];
+      t.z = pp[2];
+      t.idx = i;
+      t.cell = c;
+      J.bin_t[pos] = t;
+    } else {
+      J.bin_q[pos] = make_int2(i, c);
+    }
+  }
+}
+
+constexpr int kBinFineThreads = 1024;
+
+__global__ __launch_bounds__(kBinFineThreads) void k_bin_fine(
+    BinJob J, const GridParams *__restrict__ gp, const int *__restrict__ offs,
+    int nscan) {
+  extern __shared__ int cnt[];  // 2^shift
+  __shared__ int scratch[40];
+  const int side = blockIdx.x >= J.nb ? 1 : 0;
+  const int b = blockIdx.x - (side ? J.nb : 0);
+  const BinSide S = J.s[side];
+  const int ncell = 1 << J.shift, base = b << J.shift;
+  const int lo = offs[S.tab + b * S.nblk] - S.sub;
+  const int hi = offs[S.tab + (b + 1) * S.nblk] - S.sub;
+  for (int j = threadIdx.x; j < ncell; j += blockDim.x) cnt[j] = 0;
+  __syncthreads();
+  for (int i = lo + threadIdx.x; i < hi; i += blockDim.x) {
+    const int c = side ? J.bin_q[i].y : J.bin_t[i].cell;
+    atomicAdd(&cnt[c - base], 1);
+  }
+  __syncthreads();
+  // exclusive scan over the bucket's cells: each thread owns a contiguous run
+  const int per = ncell / blockDim.x;  // ncell is a multiple of the block size
+  const int j0 = threadIdx.x * per;
+  int sum = 0;
+  for (int u = 0; u < per; ++u) sum += cnt[j0 + u];
+  int total;
+  int acc = lo + block_excl_scan(sum, scratch, &total);
+  for (int u = 0; u < per; ++u) {
+    const int v = cnt[j0 + u];
+    cnt[j0 + u] = acc;
+    if (base + j0 + u < nscan) S.start[base + j0 + u] = acc;
+    acc += v;
+  }
+  __syncthreads();
+  const GridParams G = *gp;
+  for (int i = lo + threadIdx.x; i < hi; i += blockDim.x) {
+    if (side) {
+      const int2 e = J.bin_q[i];
+      J.qperm[atomicAdd(&cnt[e.y - base], 1)] = e.x;
+    } else {
+      const BinPt t = J.bin_t[i];
+      const int pos = atomicAdd(&cnt[t.cell - base], 1);
+      J.tsort[3 * (size_t)pos] = t.x;
+      J.tsort[3 * (size_t)pos + 1] = t.y;
+      J.tsort[3 * (size_t)pos + 2] = t.z;
+      Rec16 r;
+      r.x = (float)(t.x - G.o[0]);
+      r.y = (float)(t.y - G.o[1]);
+      r.z = (float)(t.z - G.o[2]);
+      r.idx = t.idx;
+      J.rec[pos] = r;
+    }
+  }
 }
 
 // (d, i) < (kd, ki): distance first, then index. Never true for d = inf/NaN.
@@ -1965,36 +2083,65 @@ int navgpu_knn_dev(navgpu_ctx *ctx, const double *tgt, size_t nt,
   ARG_CHECK(capl < INT32_MAX / 2);
   const int cap = (int)capl;
   const int nscan = cap + 1;  // start[] has one entry past the last cell
-  const int nb = (nscan + kScanTile - 1) / kScanTile;
-  if (nb > kScanTile) {
-    set_err("knn: %zu targets exceed the scan capacity", nt);
+  // binning geometry (k_bin_*): coarse buckets of 2^shift cells, at most
+  // kBinMaxBuckets of them; chunks of P points per histogram block
+  int shift = 10;
+  while (((long long)nscan + (1 << shift) - 1) >> shift > kBinMaxBuckets) ++shift;
+  if (shift > kBinMaxShift) {
+    set_err("knn: %zu targets exceed the binning capacity", nt);
+    return NAVGPU_ERANGE;
+  }
+  BinJob J;
+  J.shift = shift;
+  J.nb = (int)(((long long)nscan + (1 << shift) - 1) >> shift);
+  const size_t ns[2] = {nt, nq};
+  long long ntab = 0;
+  for (int side = 0; side < 2; ++side) {
+    BinSide &S = J.s[side];
+    S.n = (int)ns[side];
+    S.P = (int)std::max<size_t>(4096, (ns[side] / 2000 + 256) / 256 * 256);
+    S.nblk = (int)std::max<size_t>(1, (ns[side] + S.P - 1) / S.P);
+    S.tab = (int)ntab;
+    S.sub = side ? (int)nt : 0;
+    ntab += (long long)J.nb * S.nblk + 1;
+  }
+  const int nbs = (int)((ntab + kScanTile - 1) / kScanTile);
+  if (nbs > kScanTile) {
+    set_err("knn: binning table of %lld entries exceeds the scan capacity", ntab);
     return NAVGPU_ERANGE;
   }
   const int nparts = (int)std::min<size_t>(kBBoxBlocks, std::max<size_t>(1, grid1d(nt, 256)));
   double *part;
   GridParams *gp;
-  int *tcnt, *tstart, *qcnt, *qstart, *bsum, *tcell = nullptr, *tslot = nullptr;
-  int *qcell, *qslot, *qperm;
+  int *tab, *offs, *tstart, *qstart, *bsum, *qperm;
   Rec16 *rec = nullptr;
   double *tsort = nullptr;
+  BinPt *bin_t = nullptr;
+  int2 *bin_q;
   RC(ws(ctx, kBBox, (size_t)kBBoxBlocks * 6, &part));
   RC(ws(ctx, kParams, 1, &gp));
-  RC(ws(ctx, kCnt, 2 * (size_t)nscan, &tcnt));
-  qcnt = tcnt + nscan;
+  RC(ws(ctx, kCnt, (size_t)ntab, &tab));
+  RC(ws(ctx, kCellId, (size_t)ntab, &offs));
   RC(ws(ctx, kStart, nscan, &tstart));
   RC(ws(ctx, kQStart, nscan, &qstart));
-  RC(ws(ctx, kBSum, nb, &bsum));
+  RC(ws(ctx, kBSum, nbs, &bsum));
   if (nt) {
-    RC(ws(ctx, kCellId, nt, &tcell));
-    RC(ws(ctx, kSlotBuf, nt, &tslot));
+    RC(ws(ctx, kSlotBuf, nt, &bin_t));
     RC(ws(ctx, kRec, nt, &rec));
     RC(ws(ctx, kTSort, 3 * nt, &tsort));
   }
-  RC(ws(ctx, kQCell, nq, &qcell));
-  RC(ws(ctx, kQSlot, nq, &qslot));
+  RC(ws(ctx, kQCell, nq, &bin_q));
   RC(ws(ctx, kQPerm, nq, &qperm));
+  J.s[0].p = tgt;
+  J.s[1].p = queries;
+  J.s[0].start = tstart;
+  J.s[1].start = qstart;
+  J.bin_t = bin_t;
+  J.bin_q = bin_q;
+  J.rec = rec;
+  J.tsort = tsort;
+  J.qperm = qperm;
   hipStream_t s = ctx->stream;
-  HIP_TRY(hipMemsetAsync(tcnt, 0, 2 * 4 * (size_t)nscan, s));
   {
     TimedRegion tb(ctx, "knn_build");
     if (nt) {
@@ -2004,33 +2151,26 @@ int navgpu_knn_dev(navgpu_ctx *ctx, const double *tgt, size_t nt,
     hipLaunchKernelGGL(k_grid_params, dim3(1), dim3(256), 0, s, part, nt ? nparts : 0,
                        nt, cap, occ, nq, gp);
     CHECK_LAUNCH("k_grid_params");
-    if (nt) {
-      hipLaunchKernelGGL(k_cell_count, dim3(grid1d(nt, 256)), dim3(256), 0, s, tgt, nt,
-                         gp, tcnt, tcell, tslot);
-      CHECK_LAUNCH("k_cell_count");
-    }
-    hipLaunchKernelGGL(k_cell_count, dim3(grid1d(nq, 256)), dim3(256), 0, s, queries,
-                       nq, gp, qcnt, qcell, qslot);
-    CHECK_LAUNCH("k_cell_count(q)");
-    for (int pass = 0; pass < 2; ++pass) {
-      const int *in = pass ? qcnt : tcnt;
-      int *out = pass ? qstart : tstart;
-      hipLaunchKernelGGL(k_scan_sums, dim3(nb), dim3(kScanBlock), 0, s, in, nscan, bsum);
-      CHECK_LAUNCH("k_scan_sums");
-      hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(kScanBlock), 0, s, bsum, nb);
-      CHECK_LAUNCH("k_scan_top");
-      hipLaunchKernelGGL(k_scan_apply, dim3(nb), dim3(kScanBlock), 0, s, in, nscan,
-                         bsum, out);
-      CHECK_LAUNCH("k_scan_apply");
-    }
-    if (nt) {
-      hipLaunchKernelGGL(k_scatter_targets, dim3(grid1d(nt, 256)), dim3(256), 0, s, tgt,
-                         nt, gp, tcell, tslot, tstart, rec, tsort);
-      CHECK_LAUNCH("k_scatter_targets");
-    }
-    hipLaunchKernelGGL(k_scatter_queries, dim3(grid1d(nq, 256)), dim3(256), 0, s, nq,
-                       qcell, qslot, qstart, qperm);
-    CHECK_LAUNCH("k_scatter_queries");
+    const dim3 gb(J.s[0].nblk + J.s[1].nblk);
+    hipLaunchKernelGGL(k_bin_hist, gb, dim3(256), 0, s, J, gp, tab);
+    CHECK_LAUNCH("k_bin_hist");
+    const int ntabi = (int)ntab;
+    hipLaunchKernelGGL(k_scan_sums, dim3(nbs), dim3(kScanBlock), 0, s, tab, ntabi, bsum);
+    CHECK_LAUNCH("k_scan_sums");
+    hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(kScanBlock), 0, s, bsum, nbs);
+    CHECK_LAUNCH("k_scan_top");
+    hipLaunchKernelGGL(k_scan_apply, dim3(nbs), dim3(kScanBlock), 0, s, tab, ntabi, bsum,
+                       offs);
+    CHECK_LAUNCH("k_scan_apply");
+    hipLaunchKernelGGL(k_bin_scatter, gb, dim3(256), 0, s, J, gp, (const int *)offs);
+    CHECK_LAUNCH("k_bin_scatter");
+    const size_t lds = (size_t)4 << shift;
+    if (lds > 48 * 1024)
+      HIP_TRY(hipFuncSetAttribute((const void *)k_bin_fine,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    hipLaunchKernelGGL(k_bin_fine, dim3(2 * J.nb), dim3(kBinFineThreads), lds, s, J, gp,
+                       (const int *)offs, nscan);
+    CHECK_LAUNCH("k_bin_fine");
   }
   KnnLists lists;
   int *counters;
