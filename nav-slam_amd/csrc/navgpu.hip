@@ -1085,7 +1085,11 @@ __device__ __forceinline__ void run_dydz(int r, int &dy, int &dz) {
 // ties, a neighbourhood reaching past the block, overfull runs) the query is
 // queued for k_knn_slow with the K-th distance found as its starting bound.
 // runs(r, t0, t1, g0): record range [t0, t1) of run r in the index space of
-// fetch (LDS tile or global array) and g0 = its first record's global position.
+// the fetches and g0 = the global (cell-sorted) position of record t0.
+// pair(t): packed coordinates of records t, t+1 (t even); idx(p): index of
+// record p. A run is walked in even-aligned pairs from t0 & ~1, lanes outside
+// [t0, t1) masked, so the key's local id (run | position from t0 & ~1) is the
+// wave-uniform loop counter.
 constexpr int kRunOffBits = 6;  // candidates per run addressable by a key
 
 struct KnnLists {
@@ -1094,10 +1098,15 @@ struct KnnLists {
   double *slow_thr;        // their starting bound (K-th dsq upper bound)
 };
 
-template <int K, class Runs, class Fetch>
+typedef float f2 __attribute__((ext_vector_type(2)));
+struct Pair3 {
+  f2 x, y, z;
+};
+
+template <int K, class Runs, class PairF, class IdxF>
 __device__ __forceinline__ void knn_one(
     const GridParams &G, const double *__restrict__ tsort, const double qv[3],
-    const int c[3], size_t q, Runs runs, Fetch fetch,
+    const int c[3], size_t q, Runs runs, PairF pair, IdxF fidx,
     int32_t *__restrict__ oidx, double *__restrict__ odist, const KnnLists &L_) {
   NV_STAMP(ts0);
   const double qr[3] = {qv[0] - G.o[0], qv[1] - G.o[1], qv[2] - G.o[2]};
@@ -1111,38 +1120,38 @@ __device__ __forceinline__ void knn_one(
   uint32_t key[KL];
 #pragma unroll
   for (int s = 0; s < KL; ++s) key[s] = kNoKey;
-  bool overflow = false;  // a run with more than 2^kRunOffBits candidates
-  typedef float f2 __attribute__((ext_vector_type(2)));
+  bool overflow = false;  // a run longer than the key's offset field
   const f2 qx2 = {qf[0], qf[0]}, qy2 = {qf[1], qf[1]}, qz2 = {qf[2], qf[2]};
 #pragma unroll 1
   for (int r = 0; r < 9; ++r) {
     int t0, t1, g0;
     runs(r, t0, t1, g0);
-    overflow |= (t1 - t0) > (1 << kRunOffBits);
+    const int ta = t0 & ~1;
+    overflow |= (t1 - ta) > (1 << kRunOffBits);
     const uint32_t rid = (uint32_t)r << kRunOffBits;
-    // the pair being processed was read one step ahead (LDS latency hides
-    // behind the arithmetic of the previous pair)
-    Rec16 a0 = fetch(t0), a1 = fetch(t0 + 1);
-    for (int t = t0; t < t1; t += 2) {
-      const Rec16 c0 = fetch(t + 2), c1 = fetch(t + 3);  // next pair
-      const f2 px = {a0.x, a1.x}, py = {a0.y, a1.y}, pz = {a0.z, a1.z};
-      const f2 fx2 = px - qx2, fy2 = py - qy2, fz2 = pz - qz2;  // packed f32
+    Pair3 a = pair(ta);  // read one step ahead of its use
+#pragma unroll 1
+    for (int u = 0; ta + u < t1; u += 2) {
+      const Pair3 nx = pair(ta + u + 2);
+      const f2 fx2 = a.x - qx2, fy2 = a.y - qy2, fz2 = a.z - qz2;  // packed f32
       const f2 d22 = __builtin_elementwise_fma(
           fz2, fz2, __builtin_elementwise_fma(fy2, fy2, fx2 * fx2));
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const float d2 = d22[j];
-        uint32_t kk = (__float_as_uint(d2) & ~kKeyMask) | rid |
-                      ((uint32_t)(t + j - t0) & ((1u << kRunOffBits) - 1));
-        if (j && t + 1 >= t1) kk = kNoKey;  // padding past the run end
+      const uint32_t lid = rid | (uint32_t)(u & ((1 << kRunOffBits) - 1));
+      uint32_t k0 = (__float_as_uint(d22[0]) & ~kKeyMask) | lid;
+      uint32_t k1 = (__float_as_uint(d22[1]) & ~kKeyMask) | (lid + 1);
+      if (ta + u < t0) k0 = kNoKey;       // before the run (odd start)
+      if (ta + u + 1 >= t1) k1 = kNoKey;  // past the run end
 #ifndef NAVGPU_DBG_NOINSERT
 #pragma unroll
-        for (int s = K; s > 0; --s) key[s] = umed3(key[s - 1], key[s], kk);
+      for (int s = K; s > 0; --s) key[s] = umed3(key[s - 1], key[s], k0);
 #endif
-        key[0] = min(key[0], kk);
-      }
-      a0 = c0;
-      a1 = c1;
+      key[0] = min(key[0], k0);
+#ifndef NAVGPU_DBG_NOINSERT
+#pragma unroll
+      for (int s = K; s > 0; --s) key[s] = umed3(key[s - 1], key[s], k1);
+#endif
+      key[0] = min(key[0], k1);
+      a = nx;
     }
   }
   NV_STAMP(ts1);
@@ -1183,8 +1192,9 @@ __device__ __forceinline__ void knn_one(
       const int r = l >> kRunOffBits, off = l & ((1 << kRunOffBits) - 1);
       int t0, t1, g0;
       runs(r, t0, t1, g0);
-      ei[s] = v ? fetch(t0 + off).idx : -1;
-      gpos[s] = g0 + off;
+      const int p = (t0 & ~1) + off;  // record, in the fetch index space
+      ei[s] = v ? fidx(p) : -1;
+      gpos[s] = g0 + (p - t0);
     }
 #pragma unroll
     for (int s = 0; s < KL; ++s) {
@@ -1282,7 +1292,10 @@ __global__ __launch_bounds__(kTileThreads, NAVGPU_KNN_MINW) void k_knn(
     const double *__restrict__ qs, const int *__restrict__ qstart,
     const int *__restrict__ qperm, int32_t *__restrict__ oidx,
     double *__restrict__ odist, KnnLists L_) {
-  __shared__ __attribute__((aligned(16))) Rec16 srec[GLOBAL ? 1 : kTileRec];
+  // pair-interleaved records: pair P = records 2P, 2P+1 as x0 x1 y0 y1 z0 z1
+  // i0 i1 (32 B), so one b128 + one b64 read gives packed operands; two
+  // spare pairs absorb the read-ahead past a run's end
+  __shared__ __attribute__((aligned(16))) float spair[GLOBAL ? 8 : (kTileRec / 2 + 2) * 8];
   __shared__ int soff[9][kTileMaxW + 4];
   __shared__ int sbase[10];
   const GridParams G = *gp;
@@ -1342,7 +1355,12 @@ __global__ __launch_bounds__(kTileThreads, NAVGPU_KNN_MINW) void k_knn(
         int r = 0;
 #pragma unroll
         for (int u = 1; u < 9; ++u) r += e >= sbase[u] ? 1 : 0;
-        srec[e] = rec[soff[r][0] + (e - sbase[r])];
+        const Rec16 v = rec[soff[r][0] + (e - sbase[r])];
+        float *d = spair + (e >> 1) * 8 + (e & 1);
+        d[0] = v.x;
+        d[2] = v.y;
+        d[4] = v.z;
+        d[6] = __int_as_float(v.idx);
       }
       __syncthreads();
     }
@@ -1365,14 +1383,33 @@ __global__ __launch_bounds__(kTileThreads, NAVGPU_KNN_MINW) void k_knn(
                      t0 = g0 + sh;
                      t1 = soff[r][i + 3] + sh;
                    },
-                   [&](int p) { return srec[min(p, kTileRec - 1)]; }, oidx, odist, L_);
+                   [&](int t) {
+                     const float *b = spair + (t >> 1) * 8;
+                     const float4 xy = *(const float4 *)b;
+                     const float2 zz = *(const float2 *)(b + 4);
+                     Pair3 P;
+                     P.x = f2{xy.x, xy.y};
+                     P.y = f2{xy.z, xy.w};
+                     P.z = f2{zz.x, zz.y};
+                     return P;
+                   },
+                   [&](int p) { return __float_as_int(spair[(p >> 1) * 8 + 6 + (p & 1)]); },
+                   oidx, odist, L_);
       } else {
         knn_one<K>(G, tsort, qv, c, q,
                    [&](int r, int &t0, int &t1, int &g0) {
                      t0 = g0 = soff[r][i];
                      t1 = soff[r][i + 3];
                    },
-                   [&](int p) { return rec[min(p, ntm1)]; }, oidx, odist, L_);
+                   [&](int t) {
+                     const Rec16 a = rec[min(t, ntm1)], b = rec[min(t + 1, ntm1)];
+                     Pair3 P;
+                     P.x = f2{a.x, b.x};
+                     P.y = f2{a.y, b.y};
+                     P.z = f2{a.z, b.z};
+                     return P;
+                   },
+                   [&](int p) { return rec[p].idx; }, oidx, odist, L_);
       }
     }
     NV_STAMP(tb2);
@@ -1401,11 +1438,67 @@ __device__ __forceinline__ void knn_insert(double *kd, int *ki, double d, int id
   }
 }
 
-// The queries k_knn could not certify, one WAVE per query: exact ring search
-// from the recorded starting bound. Each ring's cells are split over the 64
-// lanes (f32 screen, then the reference f64 distance), each lane keeps its
-// own sorted list, and after every ring the lists are merged by K rounds of a
-// 64-lane (distance, index) argmin; the merged K-th bounds the next ring.
+// merge the 64 lane lists kd/ki (each sorted) into md/mi: K rounds of a
+// wave (distance, index) argmin on the list heads
+template <int K>
+__device__ __forceinline__ void knn_wave_merge(double *kd, int *ki, double *md, int *mi,
+                                               int lane) {
+#pragma unroll
+  for (int s = 0; s < K; ++s) {
+    double bd = kd[0];
+    int bi = ki[0], bl = lane;
+#pragma unroll
+    for (int o = kWave / 2; o > 0; o >>= 1) {
+      const double od = __shfl_xor(bd, o, kWave);
+      const int oi = __shfl_xor(bi, o, kWave), ol = __shfl_xor(bl, o, kWave);
+      const bool take = knn_less(od, oi, bd, bi) ||
+                        (!knn_less(bd, bi, od, oi) && ol < bl);
+      bd = take ? od : bd;
+      bi = take ? oi : bi;
+      bl = take ? ol : bl;
+    }
+    md[s] = bd;
+    mi[s] = bi;
+    if (lane == bl) {  // pop the winner's head
+#pragma unroll
+      for (int u = 0; u < K - 1; ++u) {
+        kd[u] = kd[u + 1];
+        ki[u] = ki[u + 1];
+      }
+      kd[K - 1] = INFINITY;
+      ki[K - 1] = -1;
+    }
+  }
+}
+
+// f32 screen + exact f64 distance of record t against the query; inserts
+// into the lane's sorted list when within thr
+template <int K>
+__device__ __forceinline__ void knn_visit(const Rec16 &rr, size_t t,
+                                          const double *__restrict__ tsort,
+                                          const double qv[3], const float qf[3],
+                                          double thr, float thr_f, double *kd, int *ki) {
+  const float fx = rr.x - qf[0], fy = rr.y - qf[1], fz = rr.z - qf[2];
+  const float d2f = __builtin_fmaf(fz, fz, __builtin_fmaf(fy, fy, fx * fx));
+  if (!(d2f <= thr_f)) return;
+  const double *tp = tsort + 3 * t;
+  const double ddx = tp[0] - qv[0], ddy = tp[1] - qv[1], ddz = tp[2] - qv[2];
+  const double dsq = ddx * ddx + ddy * ddy + ddz * ddz;  // utils/kdtree.c:16
+  if (!(dsq <= thr)) return;
+  knn_insert<K>(kd, ki, __builtin_sqrt(dsq), rr.idx);
+}
+
+constexpr int kSlowMaxR = 3;  // one-shot cube: at most (2R+1)^2 = 49 rows
+
+// The queries k_knn could not certify, one WAVE per query, from the recorded
+// starting bound thr (K real points lie within it, so every neighbour does).
+// One-shot cube: the smallest cube of cells around the query whose outside is
+// provably beyond thr; its (y, z) rows are contiguous record ranges, counted
+// and prefix-summed across the wave so the records are dealt evenly over the
+// 64 lanes. Each lane keeps a sorted list (f32 screen, then the reference f64
+// distance); one wave merge gives the answer. An infinite bound, or a cube
+// beyond kSlowMaxR, takes the ring search: rings of cells split over the
+// lanes, merged after every ring, the merged K-th bounding the next ring.
 template <int K>
 __global__ __launch_bounds__(256) void k_knn_slow(
     const GridParams *__restrict__ gp, const int *__restrict__ start,
@@ -1437,7 +1530,64 @@ __global__ __launch_bounds__(256) void k_knn_slow(
       kd[s] = INFINITY;
       ki[s] = -1;
     }
-    for (int r = 0; r <= gmax; ++r) {
+    // cube radius: everything outside cube R is at least L_R away
+    int R = -1;
+    if (thr < INFINITY) {
+      for (int r = 1; r <= kSlowMaxR; ++r) {
+        double L = INFINITY;
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+          if (c[a] - r > 0) L = fmin(L, qv[a] - (G.o[a] + (c[a] - r) * G.h));
+          if (c[a] + r < G.g[a] - 1) L = fmin(L, (G.o[a] + (c[a] + r + 1) * G.h) - qv[a]);
+        }
+        const double Lg = L - 2.0 * G.delta;
+        if (L == INFINITY || (Lg > 0.0 && thr < Lg * Lg)) {
+          R = r;
+          break;
+        }
+      }
+    }
+    if (R > 0) {
+      const int xl = max(c[0] - R, 0), xh = min(c[0] + R, G.g[0] - 1);
+      const int yl = max(c[1] - R, 0), yh = min(c[1] + R, G.g[1] - 1);
+      const int zl = max(c[2] - R, 0), zh = min(c[2] + R, G.g[2] - 1);
+      const int ny = yh - yl + 1, nrows = ny * (zh - zl + 1);  // <= 49
+      int cnt = 0, b = 0;
+      if (lane < nrows) {
+        const int y = yl + lane % ny, z = zl + lane / ny;
+        if (!(box_d2(G, qv, xl, xh, y, y, z, z) > thr)) {
+          const int row = (z * G.g[1] + y) * G.g[0];
+          b = start[row + xl];
+          cnt = start[row + xh + 1] - b;
+        }
+      }
+      int pre = cnt;  // inclusive wave scan of the row counts
+#pragma unroll
+      for (int o = 1; o < kWave; o <<= 1) {
+        const int t = __shfl_up(pre, o, kWave);
+        if (lane >= o) pre += t;
+      }
+      const int total = __shfl(pre, kWave - 1, kWave);
+      pre -= cnt;  // exclusive
+      for (int j0 = 0; j0 < total; j0 += kWave) {
+        const int j = j0 + lane;
+        // row of flattened record j: the last row whose prefix is <= j
+        int lo = 0;
+#pragma unroll
+        for (int step = 32; step > 0; step >>= 1) {
+          const int cand = lo + step;
+          const int pc = __shfl(pre, cand < nrows ? cand : 0, kWave);
+          if (cand < nrows && pc <= j) lo = cand;
+        }
+        const int pb = __shfl(b, lo, kWave), pp = __shfl(pre, lo, kWave);
+        if (j < total) {
+          const size_t t = (size_t)(pb + (j - pp));
+          knn_visit<K>(rec[t], t, tsort, qv, qf, thr, thr_f, kd, ki);
+        }
+      }
+      knn_wave_merge<K>(kd, ki, md, mi, lane);
+    }
+    for (int r = 0; R < 0 && r <= gmax; ++r) {
       // the ring's cube clipped to the grid (a degenerate axis stays 1 thick)
       const int xl = max(c[0] - r, 0), xh = min(c[0] + r, G.g[0] - 1);
       const int yl = max(c[1] - r, 0), yh = min(c[1] + r, G.g[1] - 1);
@@ -1450,45 +1600,10 @@ __global__ __launch_bounds__(256) void k_knn_slow(
         if (box_d2(G, qv, x, x, y, y, z, z) > thr) continue;
         const int cell = (z * G.g[1] + y) * G.g[0] + x;
         const int b = start[cell], en = start[cell + 1];
-        for (int t = b; t < en; ++t) {
-          const Rec16 rr = rec[t];
-          const float fx = rr.x - qf[0], fy = rr.y - qf[1], fz = rr.z - qf[2];
-          const float d2f = __builtin_fmaf(fz, fz, __builtin_fmaf(fy, fy, fx * fx));
-          if (!(d2f <= thr_f)) continue;
-          const double *tp = tsort + 3 * (size_t)t;
-          const double ddx = tp[0] - qv[0], ddy = tp[1] - qv[1], ddz = tp[2] - qv[2];
-          const double dsq = ddx * ddx + ddy * ddy + ddz * ddz;
-          if (!(dsq <= thr)) continue;
-          knn_insert<K>(kd, ki, __builtin_sqrt(dsq), rr.idx);
-        }
+        for (int t = b; t < en; ++t)
+          knn_visit<K>(rec[t], (size_t)t, tsort, qv, qf, thr, thr_f, kd, ki);
       }
-      // merge the 64 lane lists: K rounds of a wave argmin on the list heads
-#pragma unroll
-      for (int s = 0; s < K; ++s) {
-        double bd = kd[0];
-        int bi = ki[0], bl = lane;
-#pragma unroll
-        for (int o = kWave / 2; o > 0; o >>= 1) {
-          const double od = __shfl_xor(bd, o, kWave);
-          const int oi = __shfl_xor(bi, o, kWave), ol = __shfl_xor(bl, o, kWave);
-          const bool take = knn_less(od, oi, bd, bi) ||
-                            (!knn_less(bd, bi, od, oi) && ol < bl);
-          bd = take ? od : bd;
-          bi = take ? oi : bi;
-          bl = take ? ol : bl;
-        }
-        md[s] = bd;
-        mi[s] = bi;
-        if (lane == bl) {  // pop the winner's head
-#pragma unroll
-          for (int u = 0; u < K - 1; ++u) {
-            kd[u] = kd[u + 1];
-            ki[u] = ki[u + 1];
-          }
-          kd[K - 1] = INFINITY;
-          ki[K - 1] = -1;
-        }
-      }
+      knn_wave_merge<K>(kd, ki, md, mi, lane);
       // lane 0 carries the merged list into the next ring
 #pragma unroll
       for (int s = 0; s < K; ++s) {
@@ -1532,7 +1647,8 @@ struct navgpu_ctx {
   std::vector<hipEvent_t> free_ev;
   std::vector<double> tan_c, tan_r;
   int tan_R = -1, tan_C = -1;
-  double knn_occ = 3.0;  // target points per grid cell (NAVGPU_KNN_OCC)
+  double knn_occ = 5.0;  // target points per grid cell (NAVGPU_KNN_OCC)
+  int knn_blocks = 0;    // k_knn blocks per XCD, 0 = auto (NAVGPU_KNN_BLOCKS)
   bool knn_stats = false;
 };
 
@@ -1673,6 +1789,7 @@ int navgpu_create(int device, void *stream, navgpu_ctx **out) {
   navgpu_ctx *c = new navgpu_ctx();
   c->device = device;
   if (const char *st = getenv("NAVGPU_KNN_STATS")) c->knn_stats = *st && *st != '0';
+  if (const char *o = getenv("NAVGPU_KNN_BLOCKS")) c->knn_blocks = atoi(o);
   if (const char *o = getenv("NAVGPU_KNN_OCC")) {
     const double v = atof(o);
     if (v > 0.05 && v < 1000) c->knn_occ = v;
@@ -2182,8 +2299,12 @@ int navgpu_knn_dev(navgpu_ctx *ctx, const double *tgt, size_t nt,
   lists.n_slow = counters + 1;
   HIP_TRY(hipMemsetAsync(counters, 0, 16, s));
   TimedRegion tr(ctx, "knn_query");
-  // tiles are walked by a grid of 8 x nbx blocks (block b -> XCD b % 8)
-  const int nbx = (int)std::min<size_t>(256, std::max<size_t>(1, nq / 1600 + 1));
+  // tiles are walked by a grid of 8 x nbx blocks (block b -> XCD b % 8, the
+  // placement HW_REG_XCC_ID reports); more blocks than resident slots
+  // balance the uneven tiles (measured plateau from ~512 per XCD at 1M)
+  const int nbx = ctx->knn_blocks > 0
+                      ? ctx->knn_blocks
+                      : (int)std::min<size_t>(768, std::max<size_t>(1, nq / 1300 + 1));
   const dim3 g(8 * nbx), b(kTileThreads);
   const dim3 gs(std::max<unsigned>(1, std::min<unsigned>(2048, grid1d(nq, 256))));
 #define KNN_CASE(KK)                                                              \
