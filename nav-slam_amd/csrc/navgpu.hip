@@ -2306,12 +2306,13 @@ int navgpu_knn_dev(navgpu_ctx *ctx, const double *tgt, size_t nt,
                       ? ctx->knn_blocks
                       : (int)std::min<size_t>(768, std::max<size_t>(1, nq / 1300 + 1));
   const dim3 g(8 * nbx), b(kTileThreads);
+  const dim3 go(8 * std::min(nbx, 32));  // overflow tiles: rare, few blocks
   const dim3 gs(std::max<unsigned>(1, std::min<unsigned>(2048, grid1d(nq, 256))));
 #define KNN_CASE(KK)                                                              \
   case KK:                                                                        \
     hipLaunchKernelGGL((k_knn<KK, false>), g, b, 0, s, gp, tstart, rec, tsort,   \
                        queries, qstart, qperm, idx, dist, lists);                 \
-    hipLaunchKernelGGL((k_knn<KK, true>), g, b, 0, s, gp, tstart, rec, tsort,    \
+    hipLaunchKernelGGL((k_knn<KK, true>), go, b, 0, s, gp, tstart, rec, tsort,   \
                        queries, qstart, qperm, idx, dist, lists);                 \
     hipLaunchKernelGGL((k_knn_slow<KK>), gs, dim3(256), 0, s, gp, tstart, rec,    \
                        tsort, queries, idx, dist, lists);                         \
