@@ -47,7 +47,11 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-reps", type=int, default=3)
     p.add_argument("--traffic-csv", default=None,
-                   help="rocprofv3 --pmc counter_collection.csv to derive HBM bytes")
+                   help="comma-separated rocprofv3 --pmc counter_collection.csv files "
+                        "(FETCH_SIZE and WRITE_SIZE passes) to derive HBM bytes")
+    p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_k3.json"),
+                   help="per-step HBM bytes measured by scripts/round_profile.sh (PMC passes)")
+    p.add_argument("--no-traffic-json", action="store_true")
     p.add_argument("--json-out", default=None)
     return p.parse_args()
 
@@ -229,10 +233,17 @@ def main():
             ach = dom_bytes / (dom_avg_us * 1e-6) / 1e9
             traffic = None
             if a.traffic_csv:
-                traffic = traffic_from_csv(a.traffic_csv, "k_knn")
+                traffic = traffic_from_csv(a.traffic_csv.split(","), "k_knn")
+            elif not a.no_traffic_json and os.path.exists(a.traffic_json):
+                with open(a.traffic_json) as f:
+                    tj = json.load(f)
+                if tj.get("k") == a.k and tj.get("points_per_cloud") == N:
+                    traffic = tj.get("bytes_per_step")
             roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
                     "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic,
-                    "kernel": "k_knn<%d>" % a.k, "avg_us": round(dom_avg_us, 2),
+                    "kernel": ("query stage k_knn<%d,false> + k_knn<%d,true> (overflow tiles) "
+                               "+ k_knn_slow<%d>, one launch each per step" % (a.k, a.k, a.k)),
+                    "avg_us": round(dom_avg_us, 2),
                     "bytes_per_launch": dom_bytes,
                     "bytes_model": "24 B/query read + 24 B/target read + 12*k B/query out"}
         elif dom_n > 0:
@@ -273,24 +284,35 @@ def main():
     return out
 
 
-def traffic_from_csv(path, kernel_sub):
-    """Per-launch HBM bytes of `kernel_sub` from a rocprofv3 counter CSV
-    (FETCH_SIZE doubled per MI355X_MICROARCH.md §HBM, + WRITE_SIZE; KB)."""
+def traffic_from_csv(paths, kernel_sub):
+    """HBM bytes per step of the kernels whose name contains `kernel_sub`, from
+    rocprofv3 --pmc counter CSVs (FETCH_SIZE in one pass, WRITE_SIZE in another;
+    both in KB). FETCH_SIZE is doubled on gfx950 (MI355X_MICROARCH.md, HBM
+    section). Per step = total / launches of the main query kernel
+    (k_knn<..., false>), the other query-stage kernels being part of the step."""
     import csv
-    fetch, write, n = 0.0, 0.0, set()
-    with open(path) as f:
-        for r in csv.DictReader(f):
-            if kernel_sub not in r.get("Kernel_Name", ""):
-                continue
-            n.add(r.get("Dispatch_Id"))
-            v = float(r.get("Counter_Value", 0))
-            if r.get("Counter_Name") == "FETCH_SIZE":
-                fetch += v
-            elif r.get("Counter_Name") == "WRITE_SIZE":
-                write += v
-    if not n:
+    fetch, write = 0.0, 0.0
+    launches = {}
+    for path in paths:
+        with open(path) as f:
+            for r in csv.DictReader(f):
+                name = r.get("Kernel_Name", "")
+                if kernel_sub not in name:
+                    continue
+                v = float(r.get("Counter_Value", 0))
+                c = r.get("Counter_Name")
+                if c == "FETCH_SIZE":
+                    fetch += v
+                elif c == "WRITE_SIZE":
+                    write += v
+                else:
+                    continue
+                if "false>" in name:
+                    launches.setdefault(c, set()).add(r.get("Dispatch_Id"))
+    nf, nw = len(launches.get("FETCH_SIZE", ())), len(launches.get("WRITE_SIZE", ()))
+    if not nf or not nw:
         return None
-    return round((2 * fetch + write) * 1024 / len(n))
+    return round((2 * fetch / nf + write / nw) * 1024)
 
 
 if __name__ == "__main__":
