@@ -117,7 +117,7 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local if ws > 1 else 0)
     torch.cuda.set_device(dev)
-    from navslam import synth
+    from navslam import shard, synth
     from navslam.gpu import NavGpu
 
     stream = torch.cuda.current_stream(dev)
@@ -126,7 +126,8 @@ def main():
     if a.workload == "k3":
         R = a.rows or 512
         Cc = a.cols or 2048
-        src_h, tgt_h = synth.uniform_pair(R, Cc, seed_src=1 + 2 * rank, seed_tgt=2 + 2 * rank)
+        s_seed, t_seed = shard.pair_seeds(rank)
+        src_h, tgt_h = synth.uniform_pair(R, Cc, seed_src=s_seed, seed_tgt=t_seed)
         N = R * Cc
         src = torch.from_numpy(src_h).to(dev)
         tgt = torch.from_numpy(tgt_h).to(dev)
@@ -152,35 +153,39 @@ def main():
         Cc = a.cols or 2048
         N = R * Cc
         if a.workload == "k2":
-            pairs = 1
-        else:
-            pairs = max(1, a.pairs // ws)
+            lo, hi, pmax = 0, 1, 1
+        else:  # contiguous block of the batch per rank
+            lo, hi = shard.shard_pairs(a.pairs, ws, rank)
+            pmax = -(-a.pairs // ws)
+        pairs = hi - lo
         srcs, tgts = [], []
-        for p in range(pairs):
-            s_h, t_h = synth.l9_pair(R, Cc, seed=1000 * rank + p + 5)
+        for p in range(lo, hi):
+            s_h, t_h = synth.l9_pair(R, Cc, seed=p + 5)
             srcs.append(torch.from_numpy(s_h).to(dev))
             tgts.append(torch.from_numpy(t_h).to(dev))
-            if a.workload == "k4" and p >= 7:   # reuse 8 distinct pairs, cycled
+            if a.workload == "k4" and p - lo >= 7:   # 8 distinct pairs, cycled
                 break
         nd = len(srcs)
-        sm = torch.empty((pairs, R, Cc), dtype=torch.int32, device=dev)
-        tm = torch.empty((pairs, R, Cc), dtype=torch.int32, device=dev)
-        idx = torch.empty((pairs, R, Cc), dtype=torch.int32, device=dev)
-        dst = torch.empty((pairs, R, Cc), dtype=torch.float64, device=dev)
+        sm = torch.empty((pmax, R, Cc), dtype=torch.int32, device=dev)
+        tm = torch.empty((pmax, R, Cc), dtype=torch.int32, device=dev)
+        idx = torch.full((pmax, R, Cc), -1, dtype=torch.int32, device=dev)
+        dst = torch.empty((pmax, R, Cc), dtype=torch.float64, device=dev)
         gather_buf = None
         if a.workload == "k4" and ws > 1:
-            gather_buf = torch.empty((ws * pairs, R, Cc), dtype=torch.int32, device=dev)
+            gather_buf = torch.empty((ws * pmax, R, Cc), dtype=torch.int32, device=dev)
 
         def step():
             for p in range(pairs):
                 g.rows_match_dev(srcs[p % nd], tgts[p % nd], R, Cc, sm[p], tm[p], idx[p], dst[p])
             if gather_buf is not None:
-                dist.all_gather_into_tensor(gather_buf, idx)
+                shard.gather_matches(idx, gather_buf)
         # matches = feature queries actually searched (constant per pair)
         step()
         torch.cuda.synchronize()
-        matches_per_step = int((sm[: min(pairs, nd)] == 1).sum().item()) * (pairs // min(pairs, nd)) \
-            + int((sm[: pairs % min(pairs, nd)] == 1).sum().item())
+        matches_per_step = 0
+        if pairs:
+            matches_per_step = int((sm[:nd] == 1).sum().item()) * (pairs // nd) \
+                + int((sm[: pairs % nd] == 1).sum().item())
         dom = "rows_match"
         dom_bytes = None
         path_bytes = None
@@ -212,11 +217,8 @@ def main():
         dist.barrier()
     t1 = time.perf_counter()
     g.timing(False)
-    elapsed = t1 - t0
-    if ws > 1:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed = float(tt.item())
+    elapsed = shard.max_over_ranks(t1 - t0, dev)
+    job_matches = shard.sum_over_ranks(matches_per_step, dev)
     kt = {}
     for name in set(path_kernels + [dom]):
         ms, n = g.timing_read(name, reset=True)
@@ -225,7 +227,7 @@ def main():
     out = None
     if rank == 0:
         ms_per_step = 1000.0 * elapsed / a.steps
-        value = ws * matches_per_step * a.steps / elapsed
+        value = job_matches * a.steps / elapsed
         dom_ms, dom_n = kt.get(dom, (0.0, 0))
         dom_avg_us = 1000.0 * dom_ms / max(dom_n, 1)
         roof = None
