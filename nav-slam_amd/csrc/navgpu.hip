@@ -14,9 +14,11 @@
 //                    feature queries against it, one workgroup per row
 //   k_rows_build / k_rows_query  the same split in two (slam.c keeps the
 //                    target trees across frames)
-//   k_bbox, k_grid_params, k_cell_count, k_scan_*, k_scatter, k_knn<K>
-//                    global mode: radix-binned uniform grid over the target
-//                    cloud + exact k-NN, (distance, index) ordering
+//   k_bbox_partial, k_grid_params, k_bin_hist, k_scan_*, k_bin_scatter,
+//   k_bin_fine       global mode index: uniform grid over the target cloud,
+//                    both clouds counting-sorted by cell without global atomics
+//   k_knn<K>, k_knn_slow<K>
+//                    exact k-NN over that grid, (distance, index) ordering
 #include <hip/hip_runtime.h>
 
 #include <math.h>
@@ -678,11 +680,12 @@ struct GridParams {
   int tile_w;       // cells per k_knn tile along x
 };
 
+constexpr int kTileMaxW = 64;  // cells per k_knn tile along x, at most
 #ifndef NAVGPU_TILE_QUERIES
-#define NAVGPU_TILE_QUERIES 220.0  // target queries per k_knn tile
+#define NAVGPU_TILE_QUERIES 165.0  // target queries per k_knn tile
 #endif
 #ifndef NAVGPU_TILE_REC
-#define NAVGPU_TILE_REC 2048
+#define NAVGPU_TILE_REC 1600
 #endif
 
 struct __align__(16) Rec16 {  // cell-sorted target: (coords - origin) in f32
@@ -734,7 +737,10 @@ __global__ __launch_bounds__(256) void k_bbox_partial(const double *__restrict__
 __global__ __launch_bounds__(256) void k_grid_params(const double *__restrict__ part,
                                                      int nparts, size_t n, int cap,
                                                      double occ, size_t nq,
-                                                     GridParams *gp) {
+                                                     GridParams *gp, int *counters) {
+  // also resets the call's k-NN counters (overflow tiles, slow queries): one
+  // launch fewer than a memset
+  if (threadIdx.x < 4) counters[threadIdx.x] = 0;
   __shared__ double s[4][6];
   double v6[6] = {INFINITY, INFINITY, INFINITY, -INFINITY, -INFINITY, -INFINITY};
   for (int b = threadIdx.x; b < nparts; b += blockDim.x)
@@ -805,7 +811,12 @@ __global__ __launch_bounds__(256) void k_grid_params(const double *__restrict__ 
   const double occ_q = (double)nq / G.ncells, occ_t = (double)n / G.ncells;
   double w = fmin(NAVGPU_TILE_QUERIES / fmax(occ_q, 1e-9),
                   0.9 * NAVGPU_TILE_REC / (9.0 * fmax(occ_t, 1e-9)) - 2.0);
-  G.tile_w = (int)fmax(1.0, fmin(64.0, floor(w)));
+  // balanced: the fewest tiles per grid row at that width, then equal widths
+  // (a ragged last tile would pay a full staging + barrier cycle for a few
+  // cells)
+  const int wmax = (int)fmax(1.0, fmin((double)kTileMaxW, floor(w)));
+  const int tpr = (G.g[0] + wmax - 1) / wmax;
+  G.tile_w = (G.g[0] + tpr - 1) / tpr;
   *gp = G;
 }
 
@@ -1198,9 +1209,13 @@ __device__ __forceinline__ void knn_one(
     }
 #pragma unroll
     for (int s = 0; s < KL; ++s) {
+#ifdef NAVGPU_DBG_NOF64  // timing-only ablation: f32 key as the distance
+      const double dsq = (double)__uint_as_float(key[s] & ~kKeyMask) + gpos[s] * 1e-30;
+#else
       const double *tp = tsort + 3 * (size_t)gpos[s];
       const double ddx = tp[0] - qv[0], ddy = tp[1] - qv[1], ddz = tp[2] - qv[2];
       const double dsq = ddx * ddx + ddy * ddy + ddz * ddz;  // utils/kdtree.c:16
+#endif
       ed[s] = ei[s] >= 0 ? __builtin_sqrt(dsq) : INFINITY;
       // an inf/NaN distance is never a neighbour (kdtree.c:117)
       if (ei[s] >= 0 && !(ed[s] < INFINITY)) {
@@ -1241,7 +1256,8 @@ __device__ __forceinline__ void knn_one(
     ok = ok && B > dk2 * (1.0 + 0x1p-46);
   else
     ok = ok && B == INFINITY;  // fewer than K neighbours: only if all was seen
-#if defined(NAVGPU_DBG_NOINSERT) || defined(NAVGPU_DBG_NOEXACT)
+#if defined(NAVGPU_DBG_NOINSERT) || defined(NAVGPU_DBG_NOEXACT) || \
+    defined(NAVGPU_DBG_NOF64) || defined(NAVGPU_DBG_NOSTAGE)
   ok = true;  // timing-only ablation builds: never take the slow path
 #endif
   if (ok) {
@@ -1263,14 +1279,13 @@ __device__ __forceinline__ void knn_one(
 }
 
 #ifndef NAVGPU_TILE_THREADS
-#define NAVGPU_TILE_THREADS 256
+#define NAVGPU_TILE_THREADS 192  // 3 waves: a ~150-query tile fills them
 #endif
 #ifndef NAVGPU_TILE_REC
-#define NAVGPU_TILE_REC 2048
+#define NAVGPU_TILE_REC 1600
 #endif
 constexpr int kTileThreads = NAVGPU_TILE_THREADS;
 constexpr int kTileRec = NAVGPU_TILE_REC;  // records staged per tile (16 B each)
-constexpr int kTileMaxW = 64;   // cells per tile along x
 
 // Global-mode exact k-NN over tiles of W consecutive cells of one grid row.
 // A tile stages the 9 neighbouring row segments (cells xa-1 .. xb+1) of the
@@ -1286,7 +1301,12 @@ template <int K, bool GLOBAL>
 #ifndef NAVGPU_KNN_MINW
 #define NAVGPU_KNN_MINW 1
 #endif
-__global__ __launch_bounds__(kTileThreads, NAVGPU_KNN_MINW) void k_knn(
+#ifdef NAVGPU_KNN_WPE
+#define NAVGPU_KNN_ATTR __attribute__((amdgpu_waves_per_eu(NAVGPU_KNN_WPE)))
+#else
+#define NAVGPU_KNN_ATTR
+#endif
+__global__ __launch_bounds__(kTileThreads, NAVGPU_KNN_MINW) NAVGPU_KNN_ATTR void k_knn(
     const GridParams *__restrict__ gp, const int *__restrict__ start,
     const Rec16 *__restrict__ rec, const double *__restrict__ tsort,
     const double *__restrict__ qs, const int *__restrict__ qstart,
@@ -1322,27 +1342,47 @@ __global__ __launch_bounds__(kTileThreads, NAVGPU_KNN_MINW) void k_knn(
     const int y = row % G.g[1], z = row / G.g[1];
     const int xa = chunk * W, xb = min(xa + W, G.g[0]) - 1;
     const int ncell = xb - xa + 4;  // soff[r][i] = first record of cell xa-1+i
-    for (int e = threadIdx.x; e < 9 * ncell; e += blockDim.x) {
-      const int r = e / ncell, i = e % ncell;
-      int dy, dz;
-      run_dydz(r, dy, dz);
-      const int yy = y + dy, zz = z + dz;
-      int v = 0;
-      if (yy >= 0 && yy < G.g[1] && zz >= 0 && zz < G.g[2]) {
-        const int x = min(max(xa - 1 + i, 0), G.g[0]);  // x = gx: row end
-        v = start[(zz * G.g[1] + yy) * G.g[0] + x];
+    // staging is latency-bound: every thread issues all its global loads
+    // before it writes any of them to LDS
+    {
+      constexpr int U = 4;  // soff entries per thread per batch
+      const int nsoff = 9 * ncell;
+      for (int e0 = 0; e0 < nsoff; e0 += U * (int)blockDim.x) {
+        int v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const int e = e0 + u * (int)blockDim.x + (int)threadIdx.x;
+          v[u] = 0;
+          if (e < nsoff) {
+            const int r = e / ncell, i = e - r * ncell;
+            int dy, dz;
+            run_dydz(r, dy, dz);
+            const int yy = y + dy, zz = z + dz;
+            if (yy >= 0 && yy < G.g[1] && zz >= 0 && zz < G.g[2]) {
+              const int x = min(max(xa - 1 + i, 0), G.g[0]);  // x = gx: row end
+              v[u] = start[(zz * G.g[1] + yy) * G.g[0] + x];
+            }
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const int e = e0 + u * (int)blockDim.x + (int)threadIdx.x;
+          if (e < nsoff) (&soff[0][0])[(e / ncell) * (kTileMaxW + 4) + e % ncell] = v[u];
+        }
       }
-      soff[r][i] = v;
     }
     __syncthreads();
     if (!GLOBAL) {
-      if (threadIdx.x == 0) {
-        int acc = 0;
-        for (int r = 0; r < 9; ++r) {
-          sbase[r] = acc;
-          acc += soff[r][ncell - 1] - soff[r][0];
+      if (threadIdx.x < kWave) {  // row segment bases: a 9-lane prefix sum
+        const int r = threadIdx.x;
+        int len = r < 9 ? soff[r][ncell - 1] - soff[r][0] : 0;
+        int inc = len;
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) {
+          const int t = __shfl_up(inc, o, kWave);
+          if (r >= o) inc += t;
         }
-        sbase[9] = acc;
+        if (r <= 9) sbase[r] = inc - len;  // r = 9: the total
       }
       __syncthreads();
       const int total = sbase[9];
@@ -1351,16 +1391,40 @@ __global__ __launch_bounds__(kTileThreads, NAVGPU_KNN_MINW) void k_knn(
         __syncthreads();
         continue;
       }
-      for (int e = threadIdx.x; e < total; e += blockDim.x) {
-        int r = 0;
+      int sb[10], s0[9];
 #pragma unroll
-        for (int u = 1; u < 9; ++u) r += e >= sbase[u] ? 1 : 0;
-        const Rec16 v = rec[soff[r][0] + (e - sbase[r])];
-        float *d = spair + (e >> 1) * 8 + (e & 1);
-        d[0] = v.x;
-        d[2] = v.y;
-        d[4] = v.z;
-        d[6] = __int_as_float(v.idx);
+      for (int u = 0; u < 10; ++u) sb[u] = sbase[u];
+#pragma unroll
+      for (int u = 0; u < 9; ++u) s0[u] = soff[u][0] - sb[u];  // global = e + s0[r]
+      constexpr int U = 8;  // records per thread per batch
+      for (int e0 = 0; e0 < total; e0 += U * (int)blockDim.x) {
+        Rec16 v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const int e = e0 + u * (int)blockDim.x + (int)threadIdx.x;
+          if (e < total) {
+            int g = e + s0[0];
+#pragma unroll
+            for (int w = 1; w < 9; ++w) g = e >= sb[w] ? e + s0[w] : g;
+#ifdef NAVGPU_DBG_NOSTAGE  // timing-only ablation: no record loads
+            v[u].x = v[u].y = v[u].z = (float)g;
+            v[u].idx = g;
+#else
+            v[u] = rec[g];
+#endif
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const int e = e0 + u * (int)blockDim.x + (int)threadIdx.x;
+          if (e < total) {
+            float *d = spair + (e >> 1) * 8 + (e & 1);
+            d[0] = v[u].x;
+            d[2] = v[u].y;
+            d[4] = v[u].z;
+            d[6] = __int_as_float(v[u].idx);
+          }
+        }
       }
       __syncthreads();
     }
@@ -1415,6 +1479,8 @@ __global__ __launch_bounds__(kTileThreads, NAVGPU_KNN_MINW) void k_knn(
     NV_STAMP(tb2);
     NV_STAMP_ADD(2, tb1, tb2);
     __syncthreads();
+    NV_STAMP(tb3);
+    NV_STAMP_ADD(7, tb2, tb3);
   }
 }
 
@@ -2242,6 +2308,8 @@ int navgpu_knn_dev(navgpu_ctx *ctx, const double *tgt, size_t nt,
   RC(ws(ctx, kStart, nscan, &tstart));
   RC(ws(ctx, kQStart, nscan, &qstart));
   RC(ws(ctx, kBSum, nbs, &bsum));
+  int *counters;
+  RC(ws(ctx, kStats, 4, &counters));  // [n_ovf, n_slow, pad, pad], zeroed by k_grid_params
   if (nt) {
     RC(ws(ctx, kSlotBuf, nt, &bin_t));
     RC(ws(ctx, kRec, nt, &rec));
@@ -2266,7 +2334,7 @@ int navgpu_knn_dev(navgpu_ctx *ctx, const double *tgt, size_t nt,
       CHECK_LAUNCH("k_bbox_partial");
     }
     hipLaunchKernelGGL(k_grid_params, dim3(1), dim3(256), 0, s, part, nt ? nparts : 0,
-                       nt, cap, occ, nq, gp);
+                       nt, cap, occ, nq, gp, counters);
     CHECK_LAUNCH("k_grid_params");
     const dim3 gb(J.s[0].nblk + J.s[1].nblk);
     hipLaunchKernelGGL(k_bin_hist, gb, dim3(256), 0, s, J, gp, tab);
@@ -2290,14 +2358,11 @@ int navgpu_knn_dev(navgpu_ctx *ctx, const double *tgt, size_t nt,
     CHECK_LAUNCH("k_bin_fine");
   }
   KnnLists lists;
-  int *counters;
-  RC(ws(ctx, kStats, 4, &counters));  // [n_ovf, n_slow, pad, pad]
   RC(ws(ctx, kOvf, (size_t)cap + 1, &lists.ovf_tiles));
   RC(ws(ctx, kSlowQ, nq, &lists.slow_q));
   RC(ws(ctx, kSlowThr, nq, &lists.slow_thr));
   lists.n_ovf = counters;
   lists.n_slow = counters + 1;
-  HIP_TRY(hipMemsetAsync(counters, 0, 16, s));
   TimedRegion tr(ctx, "knn_query");
   // tiles are walked by a grid of 8 x nbx blocks (block b -> XCD b % 8, the
   // placement HW_REG_XCC_ID reports); more blocks than resident slots
