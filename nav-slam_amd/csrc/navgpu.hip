@@ -21,6 +21,8 @@
 //                    exact k-NN over that grid, (distance, index) ordering
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include <math.h>
 #include <stdarg.h>
 #include <stdint.h>
@@ -442,10 +444,22 @@ __device__ int row_stage_and_build(const double *feat_src, const double *coords,
 }
 
 // -------------------------------------------------------------- R1 kernel
-__global__ __launch_bounds__(kCurvTile) void k_curvature(
-    const double *__restrict__ pts, int R, int C, int32_t *__restrict__ mask,
-    double *__restrict__ curv) {
+// up to two clouds per launch (blockIdx.z); when part != nullptr the blocks
+// of cloud `part_cloud` also write the min/max of their finite coordinates
+// (the k-NN grid's bbox partials, one per block)
+struct CurvJob {
+  const double *pts[2];
+  int32_t *mask[2];
+  double *curv[2];
+  double *part;
+  int part_cloud;
+};
+
+__global__ __launch_bounds__(kCurvTile) void k_curvature(CurvJob J, int R, int C) {
   __shared__ double tile[3 * (kCurvTile + 4)];
+  __shared__ double sbb[kCurvTile / kWave][6];
+  const int z = blockIdx.z;
+  const double *pts = J.pts[z];
   const int r = blockIdx.y;
   const int c0 = blockIdx.x * kCurvTile;
   const int lo = max(0, c0 - 2), hi = min(C, c0 + kCurvTile + 2);
@@ -455,12 +469,38 @@ __global__ __launch_bounds__(kCurvTile) void k_curvature(
   for (int i = threadIdx.x; i < nd; i += kCurvTile) tile[i] = src[i];
   __syncthreads();
   const int j = c0 + threadIdx.x;
-  if (j >= C) return;
   const double *t = tile + 3 * (j - lo);
+  if (J.part && z == J.part_cloud) {  // uniform per block
+    double v6[6] = {INFINITY, INFINITY, INFINITY, -INFINITY, -INFINITY, -INFINITY};
+    if (j < C) {
+#pragma unroll
+      for (int a = 0; a < 3; ++a)
+        if (fabs(t[a]) < INFINITY) {
+          v6[a] = t[a];
+          v6[3 + a] = t[a];
+        }
+    }
+#pragma unroll
+    for (int a = 0; a < 3; ++a)
+      for (int o = kWave / 2; o > 0; o >>= 1) {
+        v6[a] = fmin(v6[a], __shfl_xor(v6[a], o, kWave));
+        v6[3 + a] = fmax(v6[3 + a], __shfl_xor(v6[3 + a], o, kWave));
+      }
+    if ((threadIdx.x & (kWave - 1)) == 0)
+      for (int a = 0; a < 6; ++a) sbb[threadIdx.x / kWave][a] = v6[a];
+    __syncthreads();
+    if (threadIdx.x < 6) {
+      const int a = threadIdx.x;
+      double v = sbb[0][a];
+      for (int w = 1; w < kCurvTile / kWave; ++w) v = a < 3 ? fmin(v, sbb[w][a]) : fmax(v, sbb[w][a]);
+      J.part[((size_t)blockIdx.y * gridDim.x + blockIdx.x) * 6 + a] = v;
+    }
+  }
+  if (j >= C) return;
   double cv = 0.0;
   if (j >= 2 && j < C - 2) cv = curvature5(t, t - 6, t - 3, t + 3, t + 6);
-  mask[rowoff + j] = cv > 0.1 ? 1 : 0;
-  if (curv) curv[rowoff + j] = cv;
+  J.mask[z][rowoff + j] = cv > 0.1 ? 1 : 0;
+  if (J.curv[z]) J.curv[z][rowoff + j] = cv;
 }
 
 // -------------------------------------------------------------- R2 kernel
@@ -986,27 +1026,41 @@ __global__ __launch_bounds__(256) void k_bin_scatter(BinJob J,
 
 constexpr int kBinFineThreads = 1024;
 
-__global__ __launch_bounds__(kBinFineThreads) void k_bin_fine(
-    BinJob J, const GridParams *__restrict__ gp, const int *__restrict__ offs,
-    int nscan) {
-  extern __shared__ int cnt[];  // 2^shift
-  __shared__ int scratch[40];
-  const int side = blockIdx.x >= J.nb ? 1 : 0;
-  const int b = blockIdx.x - (side ? J.nb : 0);
-  const BinSide S = J.s[side];
-  const int ncell = 1 << J.shift, base = b << J.shift;
-  const int lo = offs[S.tab + b * S.nblk] - S.sub;
-  const int hi = offs[S.tab + (b + 1) * S.nblk] - S.sub;
+constexpr int kBinFineHold = 4;  // points per thread held in registers
+
+// One bucket: count its points per cell (LDS), scan, write the cell starts,
+// then place every point. The first kBinFineHold * blockDim points stay in
+// registers between the count and the placement (one global read, not two);
+// a larger bucket re-reads the rest.
+template <bool QSIDE>
+__device__ void bin_fine_bucket(const BinJob &J, const BinSide &S, const GridParams *gp,
+                                int lo, int hi, int base, int ncell, int nscan, int *cnt,
+                                int *scratch) {
+  typedef typename std::conditional<QSIDE, int2, BinPt>::type E;
+  const E *src = QSIDE ? (const E *)J.bin_q : (const E *)J.bin_t;
+  auto cell_of_e = [](const E &e) {
+    if constexpr (QSIDE) return e.y; else return e.cell;
+  };
   for (int j = threadIdx.x; j < ncell; j += blockDim.x) cnt[j] = 0;
   __syncthreads();
-  for (int i = lo + threadIdx.x; i < hi; i += blockDim.x) {
-    const int c = side ? J.bin_q[i].y : J.bin_t[i].cell;
-    atomicAdd(&cnt[c - base], 1);
+  E hold[kBinFineHold];
+  const int bd = (int)blockDim.x, held_end = min(hi, lo + kBinFineHold * bd);
+#pragma unroll
+  for (int u = 0; u < kBinFineHold; ++u) {
+    const int i = lo + u * bd + (int)threadIdx.x;
+    if (i < held_end) hold[u] = src[i];
   }
+#pragma unroll
+  for (int u = 0; u < kBinFineHold; ++u) {
+    const int i = lo + u * bd + (int)threadIdx.x;
+    if (i < held_end) atomicAdd(&cnt[cell_of_e(hold[u]) - base], 1);
+  }
+  for (int i = held_end + (int)threadIdx.x; i < hi; i += bd)
+    atomicAdd(&cnt[cell_of_e(src[i]) - base], 1);
   __syncthreads();
   // exclusive scan over the bucket's cells: each thread owns a contiguous run
-  const int per = ncell / blockDim.x;  // ncell is a multiple of the block size
-  const int j0 = threadIdx.x * per;
+  const int per = ncell / bd;  // ncell is a multiple of the block size
+  const int j0 = (int)threadIdx.x * per;
   int sum = 0;
   for (int u = 0; u < per; ++u) sum += cnt[j0 + u];
   int total;
@@ -1019,24 +1073,45 @@ __global__ __launch_bounds__(kBinFineThreads) void k_bin_fine(
   }
   __syncthreads();
   const GridParams G = *gp;
-  for (int i = lo + threadIdx.x; i < hi; i += blockDim.x) {
-    if (side) {
-      const int2 e = J.bin_q[i];
+  auto place = [&](const E &e) {
+    if constexpr (QSIDE) {
       J.qperm[atomicAdd(&cnt[e.y - base], 1)] = e.x;
     } else {
-      const BinPt t = J.bin_t[i];
-      const int pos = atomicAdd(&cnt[t.cell - base], 1);
-      J.tsort[3 * (size_t)pos] = t.x;
-      J.tsort[3 * (size_t)pos + 1] = t.y;
-      J.tsort[3 * (size_t)pos + 2] = t.z;
+      const int pos = atomicAdd(&cnt[e.cell - base], 1);
+      J.tsort[3 * (size_t)pos] = e.x;
+      J.tsort[3 * (size_t)pos + 1] = e.y;
+      J.tsort[3 * (size_t)pos + 2] = e.z;
       Rec16 r;
-      r.x = (float)(t.x - G.o[0]);
-      r.y = (float)(t.y - G.o[1]);
-      r.z = (float)(t.z - G.o[2]);
-      r.idx = t.idx;
+      r.x = (float)(e.x - G.o[0]);
+      r.y = (float)(e.y - G.o[1]);
+      r.z = (float)(e.z - G.o[2]);
+      r.idx = e.idx;
       J.rec[pos] = r;
     }
+  };
+#pragma unroll
+  for (int u = 0; u < kBinFineHold; ++u) {
+    const int i = lo + u * bd + (int)threadIdx.x;
+    if (i < held_end) place(hold[u]);
   }
+  for (int i = held_end + (int)threadIdx.x; i < hi; i += bd) place(src[i]);
+}
+
+__global__ __launch_bounds__(kBinFineThreads) void k_bin_fine(
+    BinJob J, const GridParams *__restrict__ gp, const int *__restrict__ offs,
+    int nscan) {
+  extern __shared__ int cnt[];  // 2^shift
+  __shared__ int scratch[40];
+  const int side = blockIdx.x >= J.nb ? 1 : 0;
+  const int b = blockIdx.x - (side ? J.nb : 0);
+  const BinSide S = J.s[side];
+  const int ncell = 1 << J.shift, base = b << J.shift;
+  const int lo = offs[S.tab + b * S.nblk] - S.sub;
+  const int hi = offs[S.tab + (b + 1) * S.nblk] - S.sub;
+  if (side)
+    bin_fine_bucket<true>(J, S, gp, lo, hi, base, ncell, nscan, cnt, scratch);
+  else
+    bin_fine_bucket<false>(J, S, gp, lo, hi, base, ncell, nscan, cnt, scratch);
 }
 
 // (d, i) < (kd, ki): distance first, then index. Never true for d = inf/NaN.
@@ -1985,9 +2060,9 @@ int navgpu_curvature_dev(navgpu_ctx *ctx, const double *pts, int R, int C,
   if ((size_t)R * C == 0) return NAVGPU_OK;
   ARG_CHECK(pts && mask);
   TimedRegion tr(ctx, "curvature");
-  dim3 grid((C + kCurvTile - 1) / kCurvTile, R);
-  hipLaunchKernelGGL(k_curvature, grid, dim3(kCurvTile), 0, ctx->stream, pts,
-                     R, C, mask, curv);
+  CurvJob J = {{pts, nullptr}, {mask, nullptr}, {curv, nullptr}, nullptr, 0};
+  dim3 grid((C + kCurvTile - 1) / kCurvTile, R, 1);
+  hipLaunchKernelGGL(k_curvature, grid, dim3(kCurvTile), 0, ctx->stream, J, R, C);
   CHECK_LAUNCH("k_curvature");
   return NAVGPU_OK;
 }
@@ -2254,9 +2329,14 @@ int navgpu_download(navgpu_ctx *ctx, void *dst, const void *src, size_t bytes) {
 }
 
 // ------------------------------------------------------------ global k-NN
-int navgpu_knn_dev(navgpu_ctx *ctx, const double *tgt, size_t nt,
-                   const double *queries, size_t nq, int k, int32_t *idx,
-                   double *dist) {
+}  // extern "C"
+
+// The k-NN call. pre_part / pre_nparts: bbox partials of the targets already
+// written by an earlier kernel on the stream (the pair path's curvature
+// launch), so the bbox pass is skipped.
+static int knn_run(navgpu_ctx *ctx, const double *tgt, size_t nt, const double *queries,
+                   size_t nq, int k, int32_t *idx, double *dist,
+                   const double *pre_part, int pre_nparts) {
   ARG_CHECK(ctx && k >= 1 && k <= 16);
   ARG_CHECK(nt < (size_t)INT32_MAX / 2 && nq < (size_t)INT32_MAX);
   if (!nq) return NAVGPU_OK;
@@ -2301,7 +2381,11 @@ int navgpu_knn_dev(navgpu_ctx *ctx, const double *tgt, size_t nt,
   double *tsort = nullptr;
   BinPt *bin_t = nullptr;
   int2 *bin_q;
-  RC(ws(ctx, kBBox, (size_t)kBBoxBlocks * 6, &part));
+  if (pre_part) {
+    part = const_cast<double *>(pre_part);
+  } else {
+    RC(ws(ctx, kBBox, (size_t)kBBoxBlocks * 6, &part));
+  }
   RC(ws(ctx, kParams, 1, &gp));
   RC(ws(ctx, kCnt, (size_t)ntab, &tab));
   RC(ws(ctx, kCellId, (size_t)ntab, &offs));
@@ -2329,12 +2413,13 @@ int navgpu_knn_dev(navgpu_ctx *ctx, const double *tgt, size_t nt,
   hipStream_t s = ctx->stream;
   {
     TimedRegion tb(ctx, "knn_build");
-    if (nt) {
+    if (nt && !pre_part) {
       hipLaunchKernelGGL(k_bbox_partial, dim3(nparts), dim3(256), 0, s, tgt, nt, part);
       CHECK_LAUNCH("k_bbox_partial");
     }
-    hipLaunchKernelGGL(k_grid_params, dim3(1), dim3(256), 0, s, part, nt ? nparts : 0,
-                       nt, cap, occ, nq, gp, counters);
+    hipLaunchKernelGGL(k_grid_params, dim3(1), dim3(256), 0, s, part,
+                       nt ? (pre_part ? pre_nparts : nparts) : 0, nt, cap, occ, nq, gp,
+                       counters);
     CHECK_LAUNCH("k_grid_params");
     const dim3 gb(J.s[0].nblk + J.s[1].nblk);
     hipLaunchKernelGGL(k_bin_hist, gb, dim3(256), 0, s, J, gp, tab);
@@ -2405,6 +2490,14 @@ int navgpu_knn_dev(navgpu_ctx *ctx, const double *tgt, size_t nt,
   return NAVGPU_OK;
 }
 
+extern "C" {
+
+int navgpu_knn_dev(navgpu_ctx *ctx, const double *tgt, size_t nt,
+                   const double *queries, size_t nq, int k, int32_t *idx,
+                   double *dist) {
+  return knn_run(ctx, tgt, nt, queries, nq, k, idx, dist, nullptr, 0);
+}
+
 int navgpu_knn_host(navgpu_ctx *ctx, const double *tgt, size_t nt,
                     const double *queries, size_t nq, int k, int32_t *idx,
                     double *dist) {
@@ -2433,9 +2526,22 @@ int navgpu_pair_knn_dev(navgpu_ctx *ctx, const double *src, const double *tgt,
   ARG_CHECK(ctx && R >= 0 && C >= 0);
   const size_t N = (size_t)R * C;
   if (!N) return NAVGPU_OK;
-  if (src_mask) RC(navgpu_curvature_dev(ctx, src, R, C, src_mask, nullptr));
-  if (tgt_mask) RC(navgpu_curvature_dev(ctx, tgt, R, C, tgt_mask, nullptr));
-  return navgpu_knn_dev(ctx, tgt, N, src, N, k, idx, dist);
+  ARG_CHECK(src && tgt);
+  if (!src_mask && !tgt_mask) return navgpu_knn_dev(ctx, tgt, N, src, N, k, idx, dist);
+  // one curvature launch over both clouds (the bbox stays a separate pass:
+  // folding it into this f64-bound kernel measured slower)
+  CurvJob J = {{src, tgt}, {src_mask, tgt_mask}, {nullptr, nullptr}, nullptr, -1};
+  if (!src_mask) {  // only the target: it becomes cloud 0
+    J.pts[0] = tgt;
+    J.mask[0] = tgt_mask;
+  }
+  {
+    TimedRegion tr(ctx, "curvature");
+    dim3 grid((C + kCurvTile - 1) / kCurvTile, R, (src_mask && tgt_mask) ? 2 : 1);
+    hipLaunchKernelGGL(k_curvature, grid, dim3(kCurvTile), 0, ctx->stream, J, R, C);
+    CHECK_LAUNCH("k_curvature");
+  }
+  return knn_run(ctx, tgt, N, src, N, k, idx, dist, nullptr, 0);
 }
 
 }  // extern "C"
