@@ -444,20 +444,15 @@ __device__ int row_stage_and_build(const double *feat_src, const double *coords,
 }
 
 // -------------------------------------------------------------- R1 kernel
-// up to two clouds per launch (blockIdx.z); when part != nullptr the blocks
-// of cloud `part_cloud` also write the min/max of their finite coordinates
-// (the k-NN grid's bbox partials, one per block)
+// up to two clouds per launch (blockIdx.z)
 struct CurvJob {
   const double *pts[2];
   int32_t *mask[2];
   double *curv[2];
-  double *part;
-  int part_cloud;
 };
 
 __global__ __launch_bounds__(kCurvTile) void k_curvature(CurvJob J, int R, int C) {
   __shared__ double tile[3 * (kCurvTile + 4)];
-  __shared__ double sbb[kCurvTile / kWave][6];
   const int z = blockIdx.z;
   const double *pts = J.pts[z];
   const int r = blockIdx.y;
@@ -470,32 +465,6 @@ __global__ __launch_bounds__(kCurvTile) void k_curvature(CurvJob J, int R, int C
   __syncthreads();
   const int j = c0 + threadIdx.x;
   const double *t = tile + 3 * (j - lo);
-  if (J.part && z == J.part_cloud) {  // uniform per block
-    double v6[6] = {INFINITY, INFINITY, INFINITY, -INFINITY, -INFINITY, -INFINITY};
-    if (j < C) {
-#pragma unroll
-      for (int a = 0; a < 3; ++a)
-        if (fabs(t[a]) < INFINITY) {
-          v6[a] = t[a];
-          v6[3 + a] = t[a];
-        }
-    }
-#pragma unroll
-    for (int a = 0; a < 3; ++a)
-      for (int o = kWave / 2; o > 0; o >>= 1) {
-        v6[a] = fmin(v6[a], __shfl_xor(v6[a], o, kWave));
-        v6[3 + a] = fmax(v6[3 + a], __shfl_xor(v6[3 + a], o, kWave));
-      }
-    if ((threadIdx.x & (kWave - 1)) == 0)
-      for (int a = 0; a < 6; ++a) sbb[threadIdx.x / kWave][a] = v6[a];
-    __syncthreads();
-    if (threadIdx.x < 6) {
-      const int a = threadIdx.x;
-      double v = sbb[0][a];
-      for (int w = 1; w < kCurvTile / kWave; ++w) v = a < 3 ? fmin(v, sbb[w][a]) : fmax(v, sbb[w][a]);
-      J.part[((size_t)blockIdx.y * gridDim.x + blockIdx.x) * 6 + a] = v;
-    }
-  }
   if (j >= C) return;
   double cv = 0.0;
   if (j >= 2 && j < C - 2) cv = curvature5(t, t - 6, t - 3, t + 3, t + 6);
@@ -2060,7 +2029,7 @@ int navgpu_curvature_dev(navgpu_ctx *ctx, const double *pts, int R, int C,
   if ((size_t)R * C == 0) return NAVGPU_OK;
   ARG_CHECK(pts && mask);
   TimedRegion tr(ctx, "curvature");
-  CurvJob J = {{pts, nullptr}, {mask, nullptr}, {curv, nullptr}, nullptr, 0};
+  CurvJob J = {{pts, nullptr}, {mask, nullptr}, {curv, nullptr}};
   dim3 grid((C + kCurvTile - 1) / kCurvTile, R, 1);
   hipLaunchKernelGGL(k_curvature, grid, dim3(kCurvTile), 0, ctx->stream, J, R, C);
   CHECK_LAUNCH("k_curvature");
@@ -2331,12 +2300,9 @@ int navgpu_download(navgpu_ctx *ctx, void *dst, const void *src, size_t bytes) {
 // ------------------------------------------------------------ global k-NN
 }  // extern "C"
 
-// The k-NN call. pre_part / pre_nparts: bbox partials of the targets already
-// written by an earlier kernel on the stream (the pair path's curvature
-// launch), so the bbox pass is skipped.
+// The k-NN call (navgpu_knn_dev).
 static int knn_run(navgpu_ctx *ctx, const double *tgt, size_t nt, const double *queries,
-                   size_t nq, int k, int32_t *idx, double *dist,
-                   const double *pre_part, int pre_nparts) {
+                   size_t nq, int k, int32_t *idx, double *dist) {
   ARG_CHECK(ctx && k >= 1 && k <= 16);
   ARG_CHECK(nt < (size_t)INT32_MAX / 2 && nq < (size_t)INT32_MAX);
   if (!nq) return NAVGPU_OK;
@@ -2381,11 +2347,7 @@ static int knn_run(navgpu_ctx *ctx, const double *tgt, size_t nt, const double *
   double *tsort = nullptr;
   BinPt *bin_t = nullptr;
   int2 *bin_q;
-  if (pre_part) {
-    part = const_cast<double *>(pre_part);
-  } else {
-    RC(ws(ctx, kBBox, (size_t)kBBoxBlocks * 6, &part));
-  }
+  RC(ws(ctx, kBBox, (size_t)kBBoxBlocks * 6, &part));
   RC(ws(ctx, kParams, 1, &gp));
   RC(ws(ctx, kCnt, (size_t)ntab, &tab));
   RC(ws(ctx, kCellId, (size_t)ntab, &offs));
@@ -2413,13 +2375,12 @@ static int knn_run(navgpu_ctx *ctx, const double *tgt, size_t nt, const double *
   hipStream_t s = ctx->stream;
   {
     TimedRegion tb(ctx, "knn_build");
-    if (nt && !pre_part) {
+    if (nt) {
       hipLaunchKernelGGL(k_bbox_partial, dim3(nparts), dim3(256), 0, s, tgt, nt, part);
       CHECK_LAUNCH("k_bbox_partial");
     }
-    hipLaunchKernelGGL(k_grid_params, dim3(1), dim3(256), 0, s, part,
-                       nt ? (pre_part ? pre_nparts : nparts) : 0, nt, cap, occ, nq, gp,
-                       counters);
+    hipLaunchKernelGGL(k_grid_params, dim3(1), dim3(256), 0, s, part, nt ? nparts : 0, nt,
+                       cap, occ, nq, gp, counters);
     CHECK_LAUNCH("k_grid_params");
     const dim3 gb(J.s[0].nblk + J.s[1].nblk);
     hipLaunchKernelGGL(k_bin_hist, gb, dim3(256), 0, s, J, gp, tab);
@@ -2495,7 +2456,7 @@ extern "C" {
 int navgpu_knn_dev(navgpu_ctx *ctx, const double *tgt, size_t nt,
                    const double *queries, size_t nq, int k, int32_t *idx,
                    double *dist) {
-  return knn_run(ctx, tgt, nt, queries, nq, k, idx, dist, nullptr, 0);
+  return knn_run(ctx, tgt, nt, queries, nq, k, idx, dist);
 }
 
 int navgpu_knn_host(navgpu_ctx *ctx, const double *tgt, size_t nt,
@@ -2530,7 +2491,7 @@ int navgpu_pair_knn_dev(navgpu_ctx *ctx, const double *src, const double *tgt,
   if (!src_mask && !tgt_mask) return navgpu_knn_dev(ctx, tgt, N, src, N, k, idx, dist);
   // one curvature launch over both clouds (the bbox stays a separate pass:
   // folding it into this f64-bound kernel measured slower)
-  CurvJob J = {{src, tgt}, {src_mask, tgt_mask}, {nullptr, nullptr}, nullptr, -1};
+  CurvJob J = {{src, tgt}, {src_mask, tgt_mask}, {nullptr, nullptr}};
   if (!src_mask) {  // only the target: it becomes cloud 0
     J.pts[0] = tgt;
     J.mask[0] = tgt_mask;
@@ -2541,7 +2502,7 @@ int navgpu_pair_knn_dev(navgpu_ctx *ctx, const double *src, const double *tgt,
     hipLaunchKernelGGL(k_curvature, grid, dim3(kCurvTile), 0, ctx->stream, J, R, C);
     CHECK_LAUNCH("k_curvature");
   }
-  return knn_run(ctx, tgt, N, src, N, k, idx, dist, nullptr, 0);
+  return knn_run(ctx, tgt, N, src, N, k, idx, dist);
 }
 
 }  // extern "C"
