@@ -228,59 +228,59 @@ __device__ int block_compact(int C, int *scratch, Flag flag, Write write) {
 // a chunk by pointer jumping over lanes (DESIGN.md §KD build). The final
 // layout is smalls | pivot | tape[S+1..m) with tape[S] moved to `last`.
 // ------------------------------------------------------------------------
-template <class IdxT>
+template <class IdxT, bool GMEM = false>
 __device__ void wave_nth_element(const double *key, IdxT *P, IdxT *T,
                                  int first, int last, int nth, int lane) {
+  // One wave owns [first, last]. In LDS its accesses execute in program
+  // order, so no fence is needed between chunks; P/T in global memory
+  // (GMEM, the large-n build) need one after each chunk's writes. The next
+  // chunk's P/key reads are issued before the current chunk resolves (this
+  // chunk only writes positions below the next chunk).
   while (first < last) {
     const int pe = (int)P[last];
     const double pk = key[pe];
     const int m = last - first;
     int S = 0;
+    int e_n = lane < m ? (int)P[first + lane] : 0;
+    double k_n = key[e_n];
     for (int cs = 0; cs < m; cs += kWave) {
       const int p = cs + lane;
       const bool act = p < m;
-      const int e = act ? (int)P[first + p] : 0;
-      const bool small = act && ((key[e] - pk) <= 0.0);  // kdtree.c:31-43
+      const int e = e_n;
+      const bool small = act && ((k_n - pk) <= 0.0);  // kdtree.c:31-43
+      if (cs + kWave < m) {  // read ahead
+        const int pn = p + kWave;
+        e_n = pn < m ? (int)P[first + pn] : 0;
+        k_n = key[e_n];
+      }
       const unsigned long long bal = __ballot(small);
       const int sp = S + lanes_below(bal);
-      int val = e;
-      bool res = true;
-      int ptr = 0;
+      // tape value of position p: bit 31 = resolved, low bits = the value, or
+      // (unresolved) the chunk lane whose value it equals
+      unsigned w = 0x80000000u | (unsigned)e;
       if (small) {
-        if (sp < cs) {
-          val = (int)T[first + sp];
-        } else if (sp != p) {
-          res = false;
-          ptr = sp - cs;
-        }
+        if (sp < cs)
+          w = 0x80000000u | (unsigned)T[first + sp];
+        else if (sp != p)
+          w = (unsigned)(sp - cs);
       }
-      while (__ballot(!res)) {
-        const int src = res ? lane : ptr;
-        const int sval = __shfl(val, src, kWave);
-        const int sres = __shfl((int)res, src, kWave);
-        const int sptr = __shfl(ptr, src, kWave);
-        if (!res) {
-          if (sres) {
-            val = sval;
-            res = true;
-          } else {
-            ptr = sptr;
-          }
-        }
+      // pointer jumping: one shuffle per round (taking the pointee's word is
+      // right both when it is resolved and when it is a further pointer)
+      while (__ballot(!(w >> 31))) {
+        const unsigned o = __shfl(w, (w >> 31) ? lane : (int)(w & (kWave - 1)), kWave);
+        if (!(w >> 31)) w = o;
       }
-      wave_sync_mem();
-      if (act) T[first + p] = (IdxT)val;
+      if (act) T[first + p] = (IdxT)(w & 0x7fffffffu);
       if (small) P[first + sp] = (IdxT)e;
       S += __popcll(bal);
-      wave_sync_mem();
+      if (GMEM) wave_sync_mem();
     }
     for (int q = S + lane; q < m; q += kWave) {
       const int v = (int)T[first + q];
       P[q == S ? last : first + q] = (IdxT)v;
     }
-    wave_sync_mem();
     if (lane == 0) P[first + S] = (IdxT)pe;
-    wave_sync_mem();
+    wave_sync_mem();  // the pass's writes before the next pass reads P
     const int i = first + S;
     if (i == nth) break;
     if (i < nth)
@@ -290,32 +290,92 @@ __device__ void wave_nth_element(const double *key, IdxT *P, IdxT *T,
   }
 }
 
-// buildKDTree over n points, level by level: every subarray of one depth is
-// independent; waves take subarrays round-robin. Range of node k at level d
-// comes from walking its bits down from the root. Root axis = depth0 % 3
-// (kdtree.c:70, getAxis(depth)).
+// The reference nth_element (utils/kdtree.c:20-52) run serially by one lane:
+// Lomuto partition, pivot = last, `cmp <= 0` goes left.
 template <class IdxT>
+__device__ void lane_nth_element(const double *key, IdxT *P, int first, int last,
+                                 int nth) {
+  while (first < last) {
+    const IdxT pe = P[last];
+    const double pk = key[pe];
+    int i = first;
+    for (int j = first; j < last; ++j) {
+      const IdxT ej = P[j];
+      if ((key[ej] - pk) <= 0.0) {
+        P[j] = P[i];
+        P[i] = ej;
+        ++i;
+      }
+    }
+    P[last] = P[i];
+    P[i] = pe;
+    if (i == nth) return;
+    if (i < nth)
+      first = i + 1;
+    else
+      last = i - 1;
+  }
+}
+
+// [lo, hi) = node range k at `depth` below a root range [0, n): walk the
+// bits of k down from the root (node of [lo, hi) at lo + (hi - lo) / 2).
+__device__ __forceinline__ void kd_node_range(int n, int depth, int k, int &lo, int &hi) {
+  lo = 0;
+  hi = n;
+  for (int b = depth - 1; b >= 0; --b) {
+    const int mid = lo + (hi - lo) / 2;
+    if ((k >> b) & 1)
+      lo = mid + 1;
+    else
+      hi = mid;
+  }
+}
+
+constexpr int kLaneSubtree = 32;  // subarrays this short: one lane per subtree
+
+// buildKDTree over n points, level by level: every subarray of one depth is
+// independent. Long subarrays: waves take them round-robin (wave-parallel
+// partition passes). Once every subarray at a depth is at most kLaneSubtree
+// long, each lane builds whole subtrees serially, level by level inside the
+// subtree (subtrees are independent, so the order of their levels is free).
+// Root axis = depth0 % 3 (kdtree.c:70, getAxis(depth)).
+template <class IdxT, bool GMEM = false>
 __device__ void block_build_kdtree(const double *FC, size_t NS, int n,
                                    IdxT *P, IdxT *T, int depth0) {
   const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
   const int nw = blockDim.x / kWave;
   for (int i = threadIdx.x; i < n; i += blockDim.x) P[i] = (IdxT)i;
   __syncthreads();
-  for (int depth = 0; (n >> depth) >= 2; ++depth) {
+  int depth = 0;
+  for (; (n >> depth) >= 2; ++depth) {
+    if ((n >> depth) < kLaneSubtree) break;  // every range at this depth is <= n >> depth
     const double *key = FC + ((depth0 + depth) % 3) * NS;
     const int nodes = 1 << depth;
     for (int k = wid; k < nodes; k += nw) {
-      int lo = 0, hi = n;
-      for (int b = depth - 1; b >= 0; --b) {
-        const int mid = lo + (hi - lo) / 2;
-        if ((k >> b) & 1)
-          lo = mid + 1;
-        else
-          hi = mid;
-      }
+      int lo, hi;
+      kd_node_range(n, depth, k, lo, hi);
       const int len = hi - lo;
-      if (len >= 2) wave_nth_element<IdxT>(key, P, T, lo, hi - 1, lo + len / 2, lane);
+      if (len >= 2) wave_nth_element<IdxT, GMEM>(key, P, T, lo, hi - 1, lo + len / 2, lane);
     }
+    __syncthreads();
+  }
+  if (n >= 2) {
+    const int roots = 1 << depth;
+    for (int k = threadIdx.x; k < roots; k += blockDim.x) {
+      int lo0, hi0;
+      kd_node_range(n, depth, k, lo0, hi0);
+      const int m = hi0 - lo0;
+      for (int d = 0; (m >> d) >= 2; ++d) {
+        const double *key = FC + ((depth0 + depth + d) % 3) * NS;
+        for (int j = 0; j < (1 << d); ++j) {
+          int lo, hi;
+          kd_node_range(m, d, j, lo, hi);
+          if (hi - lo >= 2)
+            lane_nth_element<IdxT>(key, P, lo0 + lo, lo0 + hi - 1, lo0 + lo + (hi - lo) / 2);
+        }
+      }
+    }
+    if (GMEM) __threadfence_block();
     __syncthreads();
   }
 }
@@ -664,7 +724,7 @@ __global__ __launch_bounds__(1024) void k_kd_build_global(
     FC[a * n + e] = pts[i];
   }
   __syncthreads();
-  block_build_kdtree<uint32_t>(FC, (size_t)n, n, P, T, depth0);
+  block_build_kdtree<uint32_t, true>(FC, (size_t)n, n, P, T, depth0);
   for (size_t i = threadIdx.x; i < 3 * (size_t)n; i += blockDim.x) {
     const size_t pos = i / 3, a = i % 3;
     pts[i] = FC[a * (size_t)n + P[pos]];
