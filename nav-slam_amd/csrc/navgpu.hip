@@ -1675,6 +1675,8 @@ __global__ __launch_bounds__(256) void k_knn_slow(
     const Rec16 *__restrict__ rec, const double *__restrict__ tsort,
     const double *__restrict__ qs, int32_t *__restrict__ oidx,
     double *__restrict__ odist, KnnLists L_) {
+  __shared__ double sd[4][kWave];  // per-wave survivor buffers (256 threads)
+  __shared__ int si[4][kWave];
   const GridParams G = *gp;
   const int n = *L_.n_slow;
   const int lane = threadIdx.x & (kWave - 1);
@@ -1754,6 +1756,45 @@ __global__ __launch_bounds__(256) void k_knn_slow(
           const size_t t = (size_t)(pb + (j - pp));
           knn_visit<K>(rec[t], t, tsort, qv, qf, thr, thr_f, kd, ki);
         }
+      }
+      // the lanes' survivors (usually ~K in all): compact them into LDS and
+      // rank each by counting smaller ones; more than 64 take the merge
+      int nsv = 0;
+#pragma unroll
+      for (int u = 0; u < K; ++u) nsv += kd[u] < INFINITY ? 1 : 0;
+      int off = nsv;
+#pragma unroll
+      for (int o = 1; o < kWave; o <<= 1) {
+        const int t = __shfl_up(off, o, kWave);
+        if (lane >= o) off += t;
+      }
+      const int tot = __shfl(off, kWave - 1, kWave);
+      off -= nsv;
+      if (tot <= kWave) {
+        double *bd = sd[threadIdx.x / kWave];
+        int *bi = si[threadIdx.x / kWave];
+#pragma unroll
+        for (int u = 0; u < K; ++u)
+          if (u < nsv) {
+            bd[off + u] = kd[u];
+            bi[off + u] = ki[u];
+          }
+        wave_sync_mem();
+        if (lane < tot) {
+          const double d = bd[lane];
+          const int id = bi[lane];
+          int rank = 0;
+          for (int t = 0; t < tot; ++t) rank += knn_less(bd[t], bi[t], d, id) ? 1 : 0;
+          if (rank < K) {
+            oidx[q * K + rank] = id;
+            odist[q * K + rank] = d;
+          }
+        } else if (lane < K) {  // fewer than K survivors: empty slots
+          oidx[q * K + lane] = -1;
+          odist[q * K + lane] = INFINITY;
+        }
+        wave_sync_mem();  // the buffer is reused by this wave's next query
+        continue;
       }
       knn_wave_merge<K>(kd, ki, md, mi, lane);
     }
