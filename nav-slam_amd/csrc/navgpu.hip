@@ -1858,6 +1858,8 @@ struct navgpu_ctx {
   std::vector<hipEvent_t> free_ev;
   std::vector<double> tan_c, tan_r;
   int tan_R = -1, tan_C = -1;
+  hipStream_t aux = nullptr;                 // side stream (pair path: curvature)
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   double knn_occ = 5.0;  // target points per grid cell (NAVGPU_KNN_OCC)
   int knn_blocks = 0;    // k_knn blocks per XCD, 0 = auto (NAVGPU_KNN_BLOCKS)
   bool knn_stats = false;
@@ -1922,15 +1924,17 @@ struct TimedRegion {
     if (hipEventCreate(&e) != hipSuccess) return nullptr;
     return e;
   }
-  TimedRegion(navgpu_ctx *c, const char *n) : ctx(c), name(n) {
+  hipStream_t st;
+  TimedRegion(navgpu_ctx *c, const char *n, hipStream_t on = nullptr)
+      : ctx(c), name(n), st(on ? on : c->stream) {
     if (!ctx->timing) return;
     a = take();
     b = take();
-    if (a && b) (void)hipEventRecord(a, ctx->stream);
+    if (a && b) (void)hipEventRecord(a, st);
   }
   ~TimedRegion() {
     if (!ctx->timing || !a || !b) return;
-    (void)hipEventRecord(b, ctx->stream);
+    (void)hipEventRecord(b, st);
     ctx->ev[name].push_back({a, b});
   }
 };
@@ -2032,6 +2036,12 @@ void navgpu_destroy(navgpu_ctx *ctx) {
       (void)hipEventDestroy(pr.second);
     }
   for (auto e : ctx->free_ev) (void)hipEventDestroy(e);
+  if (ctx->aux) {
+    (void)hipStreamSynchronize(ctx->aux);
+    (void)hipStreamDestroy(ctx->aux);
+  }
+  if (ctx->ev_fork) (void)hipEventDestroy(ctx->ev_fork);
+  if (ctx->ev_join) (void)hipEventDestroy(ctx->ev_join);
   if (ctx->own_stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;
 }
@@ -2590,20 +2600,31 @@ int navgpu_pair_knn_dev(navgpu_ctx *ctx, const double *src, const double *tgt,
   if (!N) return NAVGPU_OK;
   ARG_CHECK(src && tgt);
   if (!src_mask && !tgt_mask) return navgpu_knn_dev(ctx, tgt, N, src, N, k, idx, dist);
-  // one curvature launch over both clouds (the bbox stays a separate pass:
-  // folding it into this f64-bound kernel measured slower)
+  // One curvature launch over both clouds, on a side stream forked from and
+  // joined back into the context's stream: it is f64-bound and independent
+  // of the (latency-bound) index build and query, so the two overlap.
+  if (!ctx->aux) {
+    HIP_TRY(hipStreamCreateWithFlags(&ctx->aux, hipStreamNonBlocking));
+    HIP_TRY(hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming));
+    HIP_TRY(hipEventCreateWithFlags(&ctx->ev_join, hipEventDisableTiming));
+  }
   CurvJob J = {{src, tgt}, {src_mask, tgt_mask}, {nullptr, nullptr}};
   if (!src_mask) {  // only the target: it becomes cloud 0
     J.pts[0] = tgt;
     J.mask[0] = tgt_mask;
   }
+  HIP_TRY(hipEventRecord(ctx->ev_fork, ctx->stream));
+  HIP_TRY(hipStreamWaitEvent(ctx->aux, ctx->ev_fork, 0));
   {
-    TimedRegion tr(ctx, "curvature");
+    TimedRegion tr(ctx, "curvature", ctx->aux);
     dim3 grid((C + kCurvTile - 1) / kCurvTile, R, (src_mask && tgt_mask) ? 2 : 1);
-    hipLaunchKernelGGL(k_curvature, grid, dim3(kCurvTile), 0, ctx->stream, J, R, C);
+    hipLaunchKernelGGL(k_curvature, grid, dim3(kCurvTile), 0, ctx->aux, J, R, C);
     CHECK_LAUNCH("k_curvature");
   }
-  return knn_run(ctx, tgt, N, src, N, k, idx, dist);
+  HIP_TRY(hipEventRecord(ctx->ev_join, ctx->aux));
+  const int rc = knn_run(ctx, tgt, N, src, N, k, idx, dist);
+  HIP_TRY(hipStreamWaitEvent(ctx->stream, ctx->ev_join, 0));  // join before returning
+  return rc;
 }
 
 }  // extern "C"
