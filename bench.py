@@ -45,6 +45,8 @@ def parse():
     p.add_argument("--cols", type=int, default=None)
     p.add_argument("--pairs", type=int, default=256, help="k4: total pairs")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--graph", action="store_true",
+                   help="k3: capture one step into a hipGraph and replay it")
     p.add_argument("--cpu-reps", type=int, default=3)
     p.add_argument("--traffic-csv", default=None,
                    help="comma-separated rocprofv3 --pmc counter_collection.csv files "
@@ -120,7 +122,9 @@ def main():
     from navslam import shard, synth
     from navslam.gpu import NavGpu
 
-    stream = torch.cuda.current_stream(dev)
+    # the library runs on a dedicated torch stream (capturable, and the one
+    # torch.cuda.synchronize() covers like any other)
+    stream = torch.cuda.Stream(dev)
     g = NavGpu(dev.index, stream.cuda_stream)
 
     if a.workload == "k3":
@@ -138,6 +142,14 @@ def main():
 
         def step():
             g.pair_knn_dev(src, tgt, R, Cc, a.k, sm, tm, idx, dst)
+        if a.graph:
+            for _ in range(2):  # warm: workspace grown, nothing allocates while capturing
+                step()
+            torch.cuda.synchronize()
+            graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(graph, stream=stream):
+                step()
+            step = graph.replay  # noqa: F811
         matches_per_step = N
         dom = "knn_query"
         dom_bytes = (24 + 24 + 12 * a.k) * N        # 24Q + 24T + 12kQ
@@ -166,6 +178,9 @@ def main():
             if a.workload == "k4" and p - lo >= 7:   # 8 distinct pairs, cycled
                 break
         nd = len(srcs)
+        if a.workload == "k4" and pairs:  # the rank's batch, resident as [pairs][R][C]
+            bsrc = torch.stack([srcs[p % nd] for p in range(pairs)])
+            btgt = torch.stack([tgts[p % nd] for p in range(pairs)])
         sm = torch.empty((pmax, R, Cc), dtype=torch.int32, device=dev)
         tm = torch.empty((pmax, R, Cc), dtype=torch.int32, device=dev)
         idx = torch.full((pmax, R, Cc), -1, dtype=torch.int32, device=dev)
@@ -175,8 +190,11 @@ def main():
             gather_buf = torch.empty((ws * pmax, R, Cc), dtype=torch.int32, device=dev)
 
         def step():
-            for p in range(pairs):
-                g.rows_match_dev(srcs[p % nd], tgts[p % nd], R, Cc, sm[p], tm[p], idx[p], dst[p])
+            if a.workload == "k4":  # one launch over the rank's whole batch
+                if pairs:
+                    g.rows_match_batch_dev(bsrc, btgt, pairs, R, Cc, sm, tm, idx, dst)
+            else:
+                g.rows_match_dev(srcs[0], tgts[0], R, Cc, sm[0], tm[0], idx[0], dst[0])
             if gather_buf is not None:
                 shard.gather_matches(idx, gather_buf)
         # matches = feature queries actually searched (constant per pair)

@@ -127,6 +127,14 @@ int navgpu_rows_match_host(navgpu_ctx *ctx, const double *src,
                            int32_t *tgt_mask, int32_t *nn_idx,
                            double *nn_dist);
 
+/* The same over a batch of independent pairs (K4), one launch: src, tgt are
+ * [npairs][R][C] clouds, masks / nn_idx / nn_dist [npairs][R][C]; nn_idx is
+ * the target index r*C+c within the query's own pair. */
+int navgpu_rows_match_batch_dev(navgpu_ctx *ctx, const double *src,
+                                const double *tgt, int npairs, int R, int C,
+                                int32_t *src_mask, int32_t *tgt_mask,
+                                int32_t *nn_idx, double *nn_dist);
+
 /* ---- Global-mode k-NN (K3) ----------------------------------------------
  * For each of nq queries the k (1..16) target points with the smallest
  * reference distance sqrt((dx*dx+dy*dy)+dz*dz), dx = target - query,

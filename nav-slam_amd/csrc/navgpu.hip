@@ -579,6 +579,8 @@ __global__ void k_transform(const double *__restrict__ pts, size_t n, Rigid g,
 }
 
 // ------------------------------------------------- fused per-row K2 kernel
+// Block = one row of a batch of pairs laid out [pair][R][C]; nn_idx is the
+// target's linear index r*C+c within its own pair.
 __global__ __launch_bounds__(kRowsBlock) void k_rows_match(
     const double *__restrict__ src, const double *__restrict__ tgt, int R,
     int C, int32_t *__restrict__ src_mask, int32_t *__restrict__ tgt_mask,
@@ -586,6 +588,7 @@ __global__ __launch_bounds__(kRowsBlock) void k_rows_match(
   const RowsLds L = rows_lds(C, kRowsBlock, true);
   const int r = blockIdx.x;
   const size_t rowoff = (size_t)r * C;
+  const int pair_row0 = (r % R) * C;  // this row's offset within its pair
   const int n = row_stage_and_build(tgt, tgt, r, C, L, tgt_mask);
   double *raw = (double *)(smem + L.raw);
   double *FC = (double *)(smem + L.fc);
@@ -629,7 +632,7 @@ __global__ __launch_bounds__(kRowsBlock) void k_rows_match(
     double bd;
     kd_query(TX, TY, TZ, n, sraw[3 * c], sraw[3 * c + 1], sraw[3 * c + 2],
              stk + threadIdx.x, blockDim.x, &bpos, &bd);
-    nn_idx[rowoff + c] = bpos >= 0 ? (int)(rowoff + T[bpos]) : -1;
+    nn_idx[rowoff + c] = bpos >= 0 ? pair_row0 + (int)T[bpos] : -1;
     nn_dist[rowoff + c] = bd;
   }
 }
@@ -2298,6 +2301,25 @@ int navgpu_rows_match_dev(navgpu_ctx *ctx, const double *src,
   RC(set_lds(k_rows_match, L.total));
   TimedRegion tr(ctx, "rows_match");
   hipLaunchKernelGGL(k_rows_match, dim3(R), dim3(kRowsBlock), L.total,
+                     ctx->stream, src, tgt, R, C, src_mask, tgt_mask, nn_idx,
+                     nn_dist);
+  CHECK_LAUNCH("k_rows_match");
+  return NAVGPU_OK;
+}
+
+int navgpu_rows_match_batch_dev(navgpu_ctx *ctx, const double *src,
+                                const double *tgt, int npairs, int R, int C,
+                                int32_t *src_mask, int32_t *tgt_mask,
+                                int32_t *nn_idx, double *nn_dist) {
+  ARG_CHECK(ctx && npairs >= 0);
+  RC(check_rows_shape(R, C, true));
+  ARG_CHECK((long long)npairs * R <= INT32_MAX && (long long)npairs * R * C < INT32_MAX);
+  if ((size_t)npairs * R * C == 0) return NAVGPU_OK;
+  ARG_CHECK(src && tgt && nn_idx && nn_dist);
+  const RowsLds L = rows_lds(C, kRowsBlock, true);
+  RC(set_lds(k_rows_match, L.total));
+  TimedRegion tr(ctx, "rows_match");
+  hipLaunchKernelGGL(k_rows_match, dim3(npairs * R), dim3(kRowsBlock), L.total,
                      ctx->stream, src, tgt, R, C, src_mask, tgt_mask, nn_idx,
                      nn_dist);
   CHECK_LAUNCH("k_rows_match");

@@ -48,6 +48,8 @@ def _declare(L):
                                             _vp, _vp, _vp, _vp]),
         "navgpu_rows_match_host": (C.c_int, [_vp, _vp, _vp, C.c_int, C.c_int,
                                              _vp, _vp, _vp, _vp]),
+        "navgpu_rows_match_batch_dev": (C.c_int, [_vp, _vp, _vp, C.c_int, C.c_int, C.c_int,
+                                                  _vp, _vp, _vp, _vp]),
         "navgpu_knn_dev": (C.c_int, [_vp, _vp, _sz, _vp, _sz, C.c_int, _vp, _vp]),
         "navgpu_knn_host": (C.c_int, [_vp, _vp, _sz, _vp, _sz, C.c_int, _vp, _vp]),
         "navgpu_pair_knn_dev": (C.c_int, [_vp, _vp, _vp, C.c_int, C.c_int, C.c_int,
@@ -234,6 +236,12 @@ class NavGpu:
         self._check(self.L.navgpu_rows_match_dev(
             self.h, _ptr(src), _ptr(tgt), R, Cc, _ptr(src_mask), _ptr(tgt_mask),
             _ptr(nn_idx), _ptr(nn_dist)), "rows_match_dev")
+
+    def rows_match_batch_dev(self, src, tgt, npairs, R, Cc, src_mask, tgt_mask, nn_idx,
+                             nn_dist):
+        self._check(self.L.navgpu_rows_match_batch_dev(
+            self.h, _ptr(src), _ptr(tgt), npairs, R, Cc, _ptr(src_mask), _ptr(tgt_mask),
+            _ptr(nn_idx), _ptr(nn_dist)), "rows_match_batch_dev")
 
     def knn_dev(self, tgt, nt, queries, nq, k, idx, dist):
         self._check(self.L.navgpu_knn_dev(self.h, _ptr(tgt), nt, _ptr(queries), nq, k,

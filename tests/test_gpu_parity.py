@@ -121,6 +121,29 @@ def test_rows_match_k2_shape_vs_oracle(gpu, orc, integer):
     assert (ref[2] >= 0).sum() > 100000
 
 
+def test_rows_match_batch_equals_per_pair(gpu, orc):
+    """K4 batch launch over [pair][R][C] == one rows_match per pair (indices
+    relative to each pair), and the oracle."""
+    import torch
+    from navslam.synth import l9_pair
+    R, Cc, P = 16, 512, 3
+    pairs = [l9_pair(R, Cc, seed=40 + p, integer_mm=p == 1) for p in range(P)]
+    dev = torch.device("cuda", 0)
+    src = torch.from_numpy(np.stack([a for a, _ in pairs])).to(dev)
+    tgt = torch.from_numpy(np.stack([b for _, b in pairs])).to(dev)
+    i32 = lambda: torch.full((P, R, Cc), -7, dtype=torch.int32, device=dev)  # noqa: E731
+    sm, tm, idx = i32(), i32(), i32()
+    dist = torch.zeros((P, R, Cc), dtype=torch.float64, device=dev)
+    gpu.rows_match_batch_dev(src, tgt, P, R, Cc, sm, tm, idx, dist)
+    torch.cuda.synchronize()
+    for p, (a, b) in enumerate(pairs):
+        ref = orc.rows_match(a, b)
+        got = (sm[p].cpu().numpy(), tm[p].cpu().numpy(), idx[p].cpu().numpy(),
+               dist[p].cpu().numpy())
+        for x, y, name in zip(got, ref, ("src_mask", "tgt_mask", "nn_idx", "nn_dist")):
+            _eq(x, y, f"pair {p} {name}")
+
+
 def test_rows_match_edge_cases(gpu, orc):
     rng = np.random.default_rng(5)
     cases = [np.zeros((3, 5, 3)),                                   # C < 5: no window
