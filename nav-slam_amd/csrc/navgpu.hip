@@ -1220,11 +1220,38 @@ typedef float f2 __attribute__((ext_vector_type(2)));
 struct Pair3 {
   f2 x, y, z;
 };
+// record cursors for knn_one: load() = packed coordinates of the current
+// pair of records, next() = the following pair
+struct LdsPairCursor {  // pair-interleaved LDS tile (x0 x1 y0 y1 z0 z1 i0 i1)
+  const float *p;
+  __device__ Pair3 load() const {
+    const float4 xy = *(const float4 *)p;
+    const float2 zz = *(const float2 *)(p + 4);
+    Pair3 P;
+    P.x = f2{xy.x, xy.y};
+    P.y = f2{xy.z, xy.w};
+    P.z = f2{zz.x, zz.y};
+    return P;
+  }
+  __device__ void next() { p += 8; }
+};
+struct RecPairCursor {  // global Rec16 array (two records of padding at its end)
+  const Rec16 *p;
+  __device__ Pair3 load() const {
+    const Rec16 a = p[0], b = p[1];
+    Pair3 P;
+    P.x = f2{a.x, b.x};
+    P.y = f2{a.y, b.y};
+    P.z = f2{a.z, b.z};
+    return P;
+  }
+  __device__ void next() { p += 2; }
+};
 
-template <int K, class Runs, class PairF, class IdxF>
+template <int K, class Runs, class CurF, class IdxF>
 __device__ __forceinline__ void knn_one(
     const GridParams &G, const double *__restrict__ tsort, const double qv[3],
-    const int c[3], size_t q, Runs runs, PairF pair, IdxF fidx,
+    const int c[3], size_t q, Runs runs, CurF cursor, IdxF fidx,
     int32_t *__restrict__ oidx, double *__restrict__ odist, const KnnLists &L_) {
   NV_STAMP(ts0);
   const double qr[3] = {qv[0] - G.o[0], qv[1] - G.o[1], qv[2] - G.o[2]};
@@ -1240,36 +1267,54 @@ __device__ __forceinline__ void knn_one(
   for (int s = 0; s < KL; ++s) key[s] = kNoKey;
   bool overflow = false;  // a run longer than the key's offset field
   const f2 qx2 = {qf[0], qf[0]}, qy2 = {qf[1], qf[1]}, qz2 = {qf[2], qf[2]};
+  auto dist2 = [&](const Pair3 &a) {  // packed f32 squared distances
+    const f2 fx2 = a.x - qx2, fy2 = a.y - qy2, fz2 = a.z - qz2;
+    return __builtin_elementwise_fma(fz2, fz2, __builtin_elementwise_fma(fy2, fy2, fx2 * fx2));
+  };
+  auto ins = [&](uint32_t kk) {  // keep the K+1 smallest keys sorted
+#ifndef NAVGPU_DBG_NOINSERT
+#pragma unroll
+    for (int s = K; s > 0; --s) key[s] = umed3(key[s - 1], key[s], kk);
+#endif
+    key[0] = min(key[0], kk);
+  };
+  constexpr uint32_t kOffMask = (1u << kRunOffBits) - 1;
 #pragma unroll 1
   for (int r = 0; r < 9; ++r) {
     int t0, t1, g0;
     runs(r, t0, t1, g0);
     const int ta = t0 & ~1;
+    const int np = (t1 - ta + 1) >> 1;  // pairs the run touches
     overflow |= (t1 - ta) > (1 << kRunOffBits);
     const uint32_t rid = (uint32_t)r << kRunOffBits;
-    Pair3 a = pair(ta);  // read one step ahead of its use
+    auto cur = cursor(ta);
+    if (np > 0) {  // first pair: may start before the run (odd t0) or end past it
+      const f2 d = dist2(cur.load());
+      uint32_t k0 = (__float_as_uint(d[0]) & ~kKeyMask) | rid;
+      uint32_t k1 = (__float_as_uint(d[1]) & ~kKeyMask) | (rid + 1);
+      if (ta < t0) k0 = kNoKey;
+      if (ta + 1 >= t1) k1 = kNoKey;
+      ins(k0);
+      ins(k1);
+      cur.next();
+    }
+    // interior pairs: both records inside the run, no masks; the key's local
+    // id is the wave-uniform pair counter
 #pragma unroll 1
-    for (int u = 0; ta + u < t1; u += 2) {
-      const Pair3 nx = pair(ta + u + 2);
-      const f2 fx2 = a.x - qx2, fy2 = a.y - qy2, fz2 = a.z - qz2;  // packed f32
-      const f2 d22 = __builtin_elementwise_fma(
-          fz2, fz2, __builtin_elementwise_fma(fy2, fy2, fx2 * fx2));
-      const uint32_t lid = rid | (uint32_t)(u & ((1 << kRunOffBits) - 1));
-      uint32_t k0 = (__float_as_uint(d22[0]) & ~kKeyMask) | lid;
-      uint32_t k1 = (__float_as_uint(d22[1]) & ~kKeyMask) | (lid + 1);
-      if (ta + u < t0) k0 = kNoKey;       // before the run (odd start)
-      if (ta + u + 1 >= t1) k1 = kNoKey;  // past the run end
-#ifndef NAVGPU_DBG_NOINSERT
-#pragma unroll
-      for (int s = K; s > 0; --s) key[s] = umed3(key[s - 1], key[s], k0);
-#endif
-      key[0] = min(key[0], k0);
-#ifndef NAVGPU_DBG_NOINSERT
-#pragma unroll
-      for (int s = K; s > 0; --s) key[s] = umed3(key[s - 1], key[s], k1);
-#endif
-      key[0] = min(key[0], k1);
-      a = nx;
+    for (int v = 1; v < np - 1; ++v) {
+      const f2 d = dist2(cur.load());
+      const uint32_t lid = rid | ((uint32_t)(2 * v) & kOffMask);
+      ins((__float_as_uint(d[0]) & ~kKeyMask) | lid);
+      ins((__float_as_uint(d[1]) & ~kKeyMask) | (lid + 1));
+      cur.next();
+    }
+    if (np > 1) {  // last pair: may end past the run
+      const f2 d = dist2(cur.load());
+      const uint32_t lid = rid | ((uint32_t)(2 * (np - 1)) & kOffMask);
+      uint32_t k1 = (__float_as_uint(d[1]) & ~kKeyMask) | (lid + 1);
+      if (ta + 2 * (np - 1) + 1 >= t1) k1 = kNoKey;
+      ins((__float_as_uint(d[0]) & ~kKeyMask) | lid);
+      ins(k1);
     }
   }
   NV_STAMP(ts1);
@@ -1540,7 +1585,6 @@ __global__ __launch_bounds__(kTileThreads, NAVGPU_KNN_MINW) NAVGPU_KNN_ATTR void
     NV_STAMP_ADD(6, 0ull, 1ull);
     const int cell0 = (z * G.g[1] + y) * G.g[0];
     const int q0 = qstart[cell0 + xa], q1 = qstart[cell0 + xb + 1];
-    const int ntm1 = max(start[G.ncells] - 1, 0);  // last valid record (prefetch clamp)
     for (int qi = q0 + threadIdx.x; qi < q1; qi += blockDim.x) {
       const size_t q = (size_t)qperm[qi];
       const double qv[3] = {qs[3 * q], qs[3 * q + 1], qs[3 * q + 2]};
@@ -1554,16 +1598,7 @@ __global__ __launch_bounds__(kTileThreads, NAVGPU_KNN_MINW) NAVGPU_KNN_ATTR void
                      t0 = g0 + sh;
                      t1 = soff[r][i + 3] + sh;
                    },
-                   [&](int t) {
-                     const float *b = spair + (t >> 1) * 8;
-                     const float4 xy = *(const float4 *)b;
-                     const float2 zz = *(const float2 *)(b + 4);
-                     Pair3 P;
-                     P.x = f2{xy.x, xy.y};
-                     P.y = f2{xy.z, xy.w};
-                     P.z = f2{zz.x, zz.y};
-                     return P;
-                   },
+                   [&](int t) { return LdsPairCursor{spair + (t >> 1) * 8}; },
                    [&](int p) { return __float_as_int(spair[(p >> 1) * 8 + 6 + (p & 1)]); },
                    oidx, odist, L_);
       } else {
@@ -1572,14 +1607,7 @@ __global__ __launch_bounds__(kTileThreads, NAVGPU_KNN_MINW) NAVGPU_KNN_ATTR void
                      t0 = g0 = soff[r][i];
                      t1 = soff[r][i + 3];
                    },
-                   [&](int t) {
-                     const Rec16 a = rec[min(t, ntm1)], b = rec[min(t + 1, ntm1)];
-                     Pair3 P;
-                     P.x = f2{a.x, b.x};
-                     P.y = f2{a.y, b.y};
-                     P.z = f2{a.z, b.z};
-                     return P;
-                   },
+                   [&](int t) { return RecPairCursor{rec + t}; },
                    [&](int p) { return rec[p].idx; }, oidx, odist, L_);
       }
     }
@@ -2491,7 +2519,7 @@ static int knn_run(navgpu_ctx *ctx, const double *tgt, size_t nt, const double *
   RC(ws(ctx, kStats, 4, &counters));  // [n_ovf, n_slow, pad, pad], zeroed by k_grid_params
   if (nt) {
     RC(ws(ctx, kSlotBuf, nt, &bin_t));
-    RC(ws(ctx, kRec, nt, &rec));
+    RC(ws(ctx, kRec, nt + 2, &rec));  // + 2: a last pair may read one past the end
     RC(ws(ctx, kTSort, 3 * nt, &tsort));
   }
   RC(ws(ctx, kQCell, nq, &bin_q));
