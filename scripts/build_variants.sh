@@ -9,10 +9,9 @@ build() {  # build <name> <defines...>
     -Iinclude "$@" -shared -o "nav-slam_amd/lib/variants/libnavgpu_$name.so" \
     nav-slam_amd/csrc/navgpu.hip &
 }
-build r2048 -DNAVGPU_TILE_REC=2048 -DNAVGPU_TILE_QUERIES=220.0
-build t192 -DNAVGPU_TILE_THREADS=192 -DNAVGPU_TILE_REC=2048 -DNAVGPU_TILE_QUERIES=165.0
-build t128 -DNAVGPU_TILE_THREADS=128 -DNAVGPU_TILE_REC=1536 -DNAVGPU_TILE_QUERIES=110.0
-build t320 -DNAVGPU_TILE_THREADS=320 -DNAVGPU_TILE_REC=3072 -DNAVGPU_TILE_QUERIES=300.0
-build t192r16 -DNAVGPU_TILE_THREADS=192 -DNAVGPU_TILE_REC=1600 -DNAVGPU_TILE_QUERIES=165.0
+build base
+build w5 -DNAVGPU_KNN_WPE=5
+build w5r1400 -DNAVGPU_KNN_WPE=5 -DNAVGPU_TILE_REC=1400 -DNAVGPU_TILE_QUERIES=150.0
+build r1800 -DNAVGPU_TILE_REC=1800 -DNAVGPU_TILE_QUERIES=165.0
 wait
 ls nav-slam_amd/lib/variants
