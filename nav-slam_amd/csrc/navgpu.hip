@@ -1056,9 +1056,15 @@ __global__ __launch_bounds__(256) void k_bin_scatter(BinJob J,
   }
 }
 
-constexpr int kBinFineThreads = 1024;
+#ifndef NAVGPU_BIN_FINE_THREADS
+#define NAVGPU_BIN_FINE_THREADS 512
+#endif
+#ifndef NAVGPU_BIN_MIN_SHIFT
+#define NAVGPU_BIN_MIN_SHIFT 9
+#endif
+constexpr int kBinFineThreads = NAVGPU_BIN_FINE_THREADS;
 
-constexpr int kBinFineHold = 4;  // points per thread held in registers
+constexpr int kBinFineHold = 4096 / kBinFineThreads;  // points per thread held in registers
 
 // One bucket: count its points per cell (LDS), scan, write the cell starts,
 // then place every point. The first kBinFineHold * blockDim points stay in
@@ -2475,7 +2481,10 @@ static int knn_run(navgpu_ctx *ctx, const double *tgt, size_t nt, const double *
   const int nscan = cap + 1;  // start[] has one entry past the last cell
   // binning geometry (k_bin_*): coarse buckets of 2^shift cells, at most
   // kBinMaxBuckets of them; chunks of P points per histogram block
-  int shift = 10;
+  // at least one cell per fine-pass thread (the fine scan gives each thread a
+  // contiguous run of 2^shift / threads cells)
+  int shift = NAVGPU_BIN_MIN_SHIFT;
+  while ((1 << shift) < kBinFineThreads) ++shift;
   while (((long long)nscan + (1 << shift) - 1) >> shift > kBinMaxBuckets) ++shift;
   if (shift > kBinMaxShift) {
     set_err("knn: %zu targets exceed the binning capacity", nt);

@@ -10,8 +10,9 @@ build() {  # build <name> <defines...>
     nav-slam_amd/csrc/navgpu.hip &
 }
 build base
-build w5 -DNAVGPU_KNN_WPE=5
-build w5r1400 -DNAVGPU_KNN_WPE=5 -DNAVGPU_TILE_REC=1400 -DNAVGPU_TILE_QUERIES=150.0
-build r1800 -DNAVGPU_TILE_REC=1800 -DNAVGPU_TILE_QUERIES=165.0
+build f512s9 -DNAVGPU_BIN_FINE_THREADS=512 -DNAVGPU_BIN_MIN_SHIFT=9
+build f256s8 -DNAVGPU_BIN_FINE_THREADS=256 -DNAVGPU_BIN_MIN_SHIFT=8
+build f512s10 -DNAVGPU_BIN_FINE_THREADS=512 -DNAVGPU_BIN_MIN_SHIFT=10
+build f256s9 -DNAVGPU_BIN_FINE_THREADS=256 -DNAVGPU_BIN_MIN_SHIFT=9
 wait
 ls nav-slam_amd/lib/variants
