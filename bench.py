@@ -109,6 +109,50 @@ def cpu_baseline_k3(src, tgt, k, reps):
                        "more)")}
 
 
+def cpu_baseline_k2(src, tgt, reps):
+    """The reference's CPU path for one per-row (slam.c) pair, rank 0 only:
+    extract_feature on both clouds (the oracle's bit-exact restatement; the
+    reference's is fixed to 8x8) + for every row the reference's own
+    buildKDTree over the target row's features and nearestNeighborSearch for
+    each source feature (oracle/_ref = utils/kdtree.c compiled as-is), which
+    is what src/slam.c:230-244 runs per frame. Single-threaded like the
+    reference; median of `reps` runs."""
+    import ctypes as C
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    from pyoracle import Oracle
+    orc = Oracle()
+    ref_path = os.path.join(ROOT, "oracle", "_ref", "libref8x8.so")
+    if not os.path.exists(ref_path):
+        return None
+    lib = C.CDLL(ref_path)
+    lib.buildKDTree.restype = C.c_void_p
+    lib.buildKDTree.argtypes = [C.c_void_p, C.c_size_t, C.c_int]
+    lib.freeKDTree.argtypes = [C.c_void_p]
+    fn = C.cast(lib.nearestNeighborSearch, C.c_void_p).value
+    R = src.shape[0]
+    times, nq = [], 0
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        sm = orc.extract_feature(src)
+        tm = orc.extract_feature(tgt)
+        nq = 0
+        for r in range(R):
+            arr = np.ascontiguousarray(tgt[r][tm[r] == 1])
+            qs = np.ascontiguousarray(src[r][sm[r] == 1])
+            nq += len(qs)
+            root = lib.buildKDTree(arr.ctypes.data, len(arr), 0)
+            if len(arr) and len(qs):
+                orc.ref_nn_batch(fn, root, qs)
+            lib.freeKDTree(root)
+        times.append(time.perf_counter() - t0)
+    t = float(np.median(times))
+    return {"value": nq / t, "unit": "matches/s", "cores": 1, "kind": "reference",
+            "seconds_per_pair": t,
+            "sample": (f"one {src.shape[0]}x{src.shape[1]} L9-shaped pair ({nq} source-feature "
+                       f"queries), median of {reps}: extract_feature x2 + per-row buildKDTree + "
+                       "nearestNeighborSearch per source feature")}
+
+
 def main():
     a = parse()
     ws, rank, local = dist_env()
@@ -205,7 +249,14 @@ def main():
             matches_per_step = int((sm[:nd] == 1).sum().item()) * (pairs // nd) \
                 + int((sm[: pairs % nd] == 1).sum().item())
         dom = "rows_match"
-        dom_bytes = None
+        # curvature 28 B per grid point of both clouds + the
+        # query stage 24 B per query + 24 B per target feature + 12 B per
+        # match (k = 1), over the pairs one launch processes
+        nmp = min(pairs, nd) if pairs else 0
+        feat_t = int((tm[:nmp] == 1).sum().item()) if nmp else 0
+        per_pair = (2 * 28 * N + 36 * (matches_per_step / max(pairs, 1))
+                    + 24 * feat_t / max(nmp, 1)) if pairs else 0
+        dom_bytes = int(per_pair * pairs) if pairs else None
         path_bytes = None
         path_kernels = ["rows_match"]
         workload = (f"{'K2' if a.workload == 'k2' else 'K4'}: {pairs} L9-shaped {R}x{Cc} "
@@ -271,6 +322,16 @@ def main():
                     "frac": None, "traffic": None, "kernel": dom,
                     "avg_us": round(dom_avg_us, 2),
                     "note": "latency/LDS-bound per-row kernel; bytes model in DESIGN.md"}
+        if a.workload != "k3" and dom_bytes and dom_n > 0:
+            ach = dom_bytes / (dom_avg_us * 1e-6) / 1e9
+            roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
+                    "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 5), "traffic": None,
+                    "kernel": "k_rows_match (fused per-row curvature + exact KD build + 1-NN)",
+                    "avg_us": round(dom_avg_us, 2), "bytes_per_launch": dom_bytes,
+                    "bytes_model": ("28 B/point x 2 clouds + 36 B/query + 24 B/target feature "
+                                    "(SURVEY 8d)"),
+                    "note": ("latency-bound: the exact reference KD permutation is a chain of "
+                             "Lomuto partition passes per row (DESIGN.md)")}
         path = None
         if path_bytes is not None:
             tot_us = 0.0
@@ -284,6 +345,9 @@ def main():
         cpu = None
         if ws == 1 and not a.no_cpu_baseline and a.workload == "k3":
             cpu = cpu_baseline_k3(src_h, tgt_h, a.k, a.cpu_reps)
+        elif rank == 0 and not a.no_cpu_baseline and a.workload in ("k2", "k4") and pairs:
+            # one pair of the batch; the reference has no batching (K4 = pairs in turn)
+            cpu = cpu_baseline_k2(srcs[0].cpu().numpy(), tgts[0].cpu().numpy(), a.cpu_reps)
         out = {"metric": METRIC, "value": round(value, 1), "unit": "matches/s",
                "n_gpus": ws, "steps": a.steps, "warmup": a.warmup,
                "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
