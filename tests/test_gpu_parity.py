@@ -217,6 +217,48 @@ def test_knn_vs_brute(gpu, orc, k):
         _eq(gd, rd, f"k={k} dist n={len(tgt)}")
 
 
+def _clustered(rng, n, centers, sigma, box):
+    c = rng.uniform(0, box, (centers, 3))
+    pts = c[rng.integers(0, centers, n)] + rng.normal(0, sigma, (n, 3))
+    return np.concatenate([pts, rng.uniform(0, box, (n // 10, 3))])
+
+
+@pytest.mark.parametrize("k", [1, 8])
+def test_knn_hard_cases(gpu, orc, k):
+    """Inputs that leave the fast path: dense clusters (LDS-overflow tiles,
+    runs longer than a key's offset field), non-finite coordinates, queries
+    far outside the target box, a large common offset."""
+    rng = np.random.default_rng(100 + k)
+    cases = []
+    # dense clusters in a sparse box: grid sized by the mean density
+    t = _clustered(rng, 20000, 6, 0.5, 1000.0)
+    q = np.concatenate([_clustered(rng, 3000, 6, 0.5, 1000.0), rng.uniform(0, 1000, (500, 3))])
+    cases.append(("clusters", t, q))
+    # non-finite targets and queries: never a neighbour / no neighbours
+    t = rng.uniform(0, 100, (3000, 3))
+    t[rng.integers(0, 3000, 40), rng.integers(0, 3, 40)] = np.nan
+    t[rng.integers(0, 3000, 40), rng.integers(0, 3, 40)] = np.inf
+    t[rng.integers(0, 3000, 20), rng.integers(0, 3, 20)] = -np.inf
+    q = rng.uniform(-10, 110, (800, 3))
+    q[rng.integers(0, 800, 30), rng.integers(0, 3, 30)] = np.nan
+    q[rng.integers(0, 800, 30), rng.integers(0, 3, 30)] = np.inf
+    cases.append(("non-finite", t, q))
+    # queries far outside the target box (every one needs the exact search)
+    t = rng.uniform(0, 100, (4000, 3))
+    q = rng.uniform(0, 100, (300, 3)) + np.array([1e5, 0, 0]) * rng.choice([-1, 1], (300, 1))
+    cases.append(("far queries", t, q))
+    # large common offset (f32 keys are relative to the grid origin)
+    off = np.array([3.7e6, -1.2e6, 9.9e5])
+    t = rng.uniform(0, 50, (4000, 3)) + off
+    q = rng.uniform(-2, 52, (1500, 3)) + off
+    cases.append(("offset", t, q))
+    for name, tgt, qs in cases:
+        ri, rd = orc.knn_brute(tgt, qs, k)
+        gi, gd = gpu.knn(tgt, qs, k)
+        _eq(gi, ri, f"{name} k={k} idx")
+        _eq(gd, rd, f"{name} k={k} dist")
+
+
 def test_knn_k1_agrees_with_reference_kd_distances(gpu, golden):
     for pts, perm, q, nn, nnd in _golden_sets(golden("kdtree")):
         if len(pts) == 0:
