@@ -290,6 +290,83 @@ __device__ void wave_nth_element(const double *key, IdxT *P, IdxT *T,
   }
 }
 
+// The reference nth_element for ONE subarray by the whole block (the top of
+// the tree, where a single wave would leave the rest of the block idle): the
+// same tape rule as wave_nth_element, one block-wide chunk of blockDim
+// positions per step. Small counts are prefix-summed across the waves;
+// tape chains that cross waves are resolved by pointer jumping through LDS
+// (bit 31 = resolved, else the chunk position whose value it equals).
+// Requires blockDim.x <= kBlockNthMax; P/T in LDS.
+constexpr int kBlockNthMax = 1024;
+template <class IdxT>
+__device__ void block_nth_element(const double *key, IdxT *P, IdxT *T, int first,
+                                  int last, int nth) {
+  __shared__ unsigned bw[kBlockNthMax];
+  __shared__ int bcnt[kBlockNthMax / kWave + 1];
+  __shared__ int bflag;
+  const int tid = threadIdx.x, lane = tid & (kWave - 1), wid = tid / kWave;
+  const int bd = blockDim.x, nw = bd / kWave;
+  while (first < last) {
+    const int pe = (int)P[last];
+    const double pk = key[pe];
+    const int m = last - first;
+    int S = 0;
+    for (int cs = 0; cs < m; cs += bd) {
+      const int p = cs + tid;
+      const bool act = p < m;
+      const int e = act ? (int)P[first + p] : 0;
+      const bool small = act && ((key[e] - pk) <= 0.0);  // kdtree.c:31-43
+      const unsigned long long bal = __ballot(small);
+      if (lane == 0) bcnt[wid] = __popcll(bal);
+      __syncthreads();
+      int before = 0, tot = 0;
+      for (int w = 0; w < nw; ++w) {
+        const int c = bcnt[w];
+        before += w < wid ? c : 0;
+        tot += c;
+      }
+      const int sp = S + before + lanes_below(bal);
+      unsigned w = 0x80000000u | (unsigned)e;
+      if (small) {
+        if (sp < cs)
+          w = 0x80000000u | (unsigned)T[first + sp];
+        else if (sp != p)
+          w = (unsigned)(sp - cs);
+      }
+      // block-wide pointer jumping
+      for (;;) {
+        bw[tid] = w;
+        if (tid == 0) bflag = 0;
+        __syncthreads();
+        if (!(w >> 31)) {
+          w = bw[w & (kBlockNthMax - 1)];
+          if (!(w >> 31)) bflag = 1;
+        }
+        __syncthreads();
+        if (!bflag) break;
+        __syncthreads();  // everyone has read bflag before it is reset
+      }
+      if (act) T[first + p] = (IdxT)(w & 0x7fffffffu);
+      if (small) P[first + sp] = (IdxT)e;
+      S += tot;
+      __syncthreads();  // this chunk's T before the next chunk reads it
+    }
+    for (int q = S + tid; q < m; q += bd) {
+      const int v = (int)T[first + q];
+      P[q == S ? last : first + q] = (IdxT)v;
+    }
+    __syncthreads();
+    if (tid == 0) P[first + S] = (IdxT)pe;
+    __syncthreads();
+    const int i = first + S;
+    if (i == nth) break;
+    if (i < nth)
+      first = i + 1;
+    else
+      last = i - 1;
+  }
+}
+
 // The reference nth_element (utils/kdtree.c:20-52) run serially by one lane:
 // Lomuto partition, pivot = last, `cmp <= 0` goes left.
 template <class IdxT>
@@ -332,6 +409,10 @@ __device__ __forceinline__ void kd_node_range(int n, int depth, int k, int &lo, 
 }
 
 constexpr int kLaneSubtree = 32;  // subarrays this short: one lane per subtree
+#ifndef NAVGPU_BLOCK_NTH_MIN
+#define NAVGPU_BLOCK_NTH_MIN 256
+#endif
+constexpr int kBlockNthMin = NAVGPU_BLOCK_NTH_MIN;  // root partition by the block from here
 
 // buildKDTree over n points, level by level: every subarray of one depth is
 // independent. Long subarrays: waves take them round-robin (wave-parallel
@@ -347,6 +428,11 @@ __device__ void block_build_kdtree(const double *FC, size_t NS, int n,
   for (int i = threadIdx.x; i < n; i += blockDim.x) P[i] = (IdxT)i;
   __syncthreads();
   int depth = 0;
+  if (!GMEM && n >= kBlockNthMin && blockDim.x <= kBlockNthMax) {
+    // the root partition by the whole block
+    block_nth_element<IdxT>(FC + (depth0 % 3) * NS, P, T, 0, n - 1, n / 2);
+    depth = 1;
+  }
   for (; (n >> depth) >= 2; ++depth) {
     if ((n >> depth) < kLaneSubtree) break;  // every range at this depth is <= n >> depth
     const double *key = FC + ((depth0 + depth) % 3) * NS;
@@ -499,7 +585,12 @@ __device__ int row_stage_and_build(const double *feat_src, const double *coords,
         FC[2 * NS + pos] = s[2];
         FCOL[pos] = (uint16_t)j;
       });
+#ifdef NAVGPU_DBG_ROWS_NOBUILD  // timing-only ablation: identity "tree"
+  for (int i = threadIdx.x; i < n; i += blockDim.x) P[i] = (uint16_t)i;
+  __syncthreads();
+#else
   block_build_kdtree<uint16_t>(FC, NS, n, P, (uint16_t *)(smem + L.t), 0);
+#endif
   return n;
 }
 
@@ -630,8 +721,13 @@ __global__ __launch_bounds__(kRowsBlock) void k_rows_match(
     const int c = QL[i];
     int bpos;
     double bd;
+#ifdef NAVGPU_DBG_ROWS_NOQUERY  // timing-only ablation
+    bpos = n ? (int)(i % n) : -1;
+    bd = sraw[3 * c];
+#else
     kd_query(TX, TY, TZ, n, sraw[3 * c], sraw[3 * c + 1], sraw[3 * c + 2],
              stk + threadIdx.x, blockDim.x, &bpos, &bd);
+#endif
     nn_idx[rowoff + c] = bpos >= 0 ? pair_row0 + (int)T[bpos] : -1;
     nn_dist[rowoff + c] = bd;
   }
@@ -1976,14 +2072,17 @@ struct TimedRegion {
   }
 };
 
+// dynamic LDS a tree-building kernel may request: the device limit minus
+// the static LDS of block_nth_element (pointer-jumping words + counts)
 int lds_limit() {
+  constexpr int kStaticLds = 4 * kBlockNthMax + 4 * (kBlockNthMax / kWave + 2) + 256;
   int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess) return 65536;
+  if (hipGetDevice(&dev) != hipSuccess) return 65536 - kStaticLds;
   int v = 0;
   if (hipDeviceGetAttribute(&v, hipDeviceAttributeMaxSharedMemoryPerBlock,
                             dev) != hipSuccess || v <= 0)
-    return 65536;
-  return v;
+    return 65536 - kStaticLds;
+  return v - kStaticLds;
 }
 
 int check_rows_shape(int R, int C, bool stack) {

@@ -10,9 +10,8 @@ build() {  # build <name> <defines...>
     nav-slam_amd/csrc/navgpu.hip &
 }
 build base
-build f512s9 -DNAVGPU_BIN_FINE_THREADS=512 -DNAVGPU_BIN_MIN_SHIFT=9
-build f256s8 -DNAVGPU_BIN_FINE_THREADS=256 -DNAVGPU_BIN_MIN_SHIFT=8
-build f512s10 -DNAVGPU_BIN_FINE_THREADS=512 -DNAVGPU_BIN_MIN_SHIFT=10
-build f256s9 -DNAVGPU_BIN_FINE_THREADS=256 -DNAVGPU_BIN_MIN_SHIFT=9
+build noblock -DNAVGPU_BLOCK_NTH_MIN=1000000
+build rows_noquery -DNAVGPU_DBG_ROWS_NOQUERY
+build noblock_noquery -DNAVGPU_BLOCK_NTH_MIN=1000000 -DNAVGPU_DBG_ROWS_NOQUERY
 wait
 ls nav-slam_amd/lib/variants

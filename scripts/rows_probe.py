@@ -8,7 +8,11 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "nav-slam_amd"))
 import torch  # noqa: E402
 from navslam import synth  # noqa: E402
+import navslam.gpu as ng  # noqa: E402
 from navslam.gpu import NavGpu  # noqa: E402
+
+if len(sys.argv) > 1:  # --lib path: an experimental build
+    ng.load_library(sys.argv[1])
 
 R, C = 128, 2048
 dev = torch.device("cuda", 0)
@@ -46,4 +50,5 @@ out = {
     "tree_n_mean": float(tn.float().mean().item()),
     "queries_mean": float(sm.float().sum(1).mean().item()),
 }
+out["lib"] = os.path.basename(sys.argv[1]) if len(sys.argv) > 1 else "libnavgpu.so"
 print(json.dumps(out))
