@@ -871,16 +871,25 @@ __global__ __launch_bounds__(256) void k_bbox_partial(const double *__restrict__
                                                       size_t n, double *__restrict__ part) {
   __shared__ double s[4][6];
   double v6[6] = {INFINITY, INFINITY, INFINITY, -INFINITY, -INFINITY, -INFINITY};
-  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
-       i += (size_t)gridDim.x * blockDim.x) {
+  // batches of 4 points per thread, all loads of a batch in flight together
+  constexpr int U = 4;
+  const size_t stride = (size_t)gridDim.x * blockDim.x;
+  for (size_t ib = (size_t)blockIdx.x * blockDim.x + threadIdx.x; ib < n; ib += U * stride) {
+    double v[U][3];
 #pragma unroll
-    for (int a = 0; a < 3; ++a) {
-      const double v = p[3 * i + a];
-      if (fabs(v) < INFINITY) {
-        v6[a] = fmin(v6[a], v);
-        v6[3 + a] = fmax(v6[3 + a], v);
-      }
+    for (int u = 0; u < U; ++u) {
+      const size_t i = ib + u * stride;
+#pragma unroll
+      for (int a = 0; a < 3; ++a) v[u][a] = i < n ? p[3 * i + a] : INFINITY;
     }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int a = 0; a < 3; ++a)
+        if (fabs(v[u][a]) < INFINITY) {
+          v6[a] = fmin(v6[a], v[u][a]);
+          v6[3 + a] = fmax(v6[3 + a], v[u][a]);
+        }
   }
 #pragma unroll
   for (int a = 0; a < 3; ++a)
@@ -1016,26 +1025,6 @@ __global__ __launch_bounds__(kScanBlock) void k_scan_sums(
   if (threadIdx.x == 0) bsum[blockIdx.x] = total;
 }
 
-__global__ __launch_bounds__(kScanBlock) void k_scan_top(int *bsum, int nb) {
-  __shared__ int scratch[40];
-  int v[kScanPer];
-  int s = 0;
-#pragma unroll
-  for (int k = 0; k < kScanPer; ++k) {
-    const int i = threadIdx.x * kScanPer + k;
-    v[k] = i < nb ? bsum[i] : 0;
-    s += v[k];
-  }
-  int total;
-  int off = block_excl_scan(s, scratch, &total);
-#pragma unroll
-  for (int k = 0; k < kScanPer; ++k) {
-    const int i = threadIdx.x * kScanPer + k;
-    if (i < nb) bsum[i] = off;
-    off += v[k];
-  }
-}
-
 __global__ __launch_bounds__(kScanBlock) void k_scan_apply(
     const int *__restrict__ in, int n, const int *__restrict__ bsum,
     int *__restrict__ out) {
@@ -1048,8 +1037,15 @@ __global__ __launch_bounds__(kScanBlock) void k_scan_apply(
     v[k] = base + k < n ? in[base + k] : 0;
     s += v[k];
   }
-  int total;
-  int off = block_excl_scan(s, scratch, &total) + bsum[blockIdx.x];
+  // this block's offset: the sum of the block totals before it, read straight
+  // from bsum (at most kScanTile of them; a separate top-level scan launch
+  // costs more than these few reads)
+  int pre = 0;
+  for (int i = threadIdx.x; i < (int)blockIdx.x; i += blockDim.x) pre += bsum[i];
+  int total, ptot;
+  block_excl_scan(pre, scratch, &ptot);
+  __syncthreads();  // scratch is reused by the next scan
+  int off = block_excl_scan(s, scratch, &total) + ptot;
 #pragma unroll
   for (int k = 0; k < kScanPer; ++k) {
     if (base + k < n) out[base + k] = off;
@@ -1104,6 +1100,37 @@ __device__ __forceinline__ int bin_side(const BinJob &J, int &blk) {
   return side;
 }
 
+#ifndef NAVGPU_BIN_UNROLL
+#define NAVGPU_BIN_UNROLL 8
+#endif
+constexpr int kBinUnroll = NAVGPU_BIN_UNROLL;  // points per thread with loads in flight
+
+struct P3 {
+  double x, y, z;
+};
+
+// the block's chunk in batches of kBinUnroll points per thread: every load of
+// a batch is issued before any of its cells is used, so a wave keeps
+// kBinUnroll x 24 B per lane in flight instead of one point's worth
+template <class F>
+__device__ __forceinline__ void bin_chunk(const BinSide &S, int blk, const GridParams &G, F f) {
+  const int i0 = blk * S.P, i1 = min(S.n, (blk + 1) * S.P);
+  const int bd = (int)blockDim.x;
+  for (int ib = i0; ib < i1; ib += kBinUnroll * bd) {
+    P3 v[kBinUnroll];
+#pragma unroll
+    for (int u = 0; u < kBinUnroll; ++u) {
+      const int i = ib + u * bd + (int)threadIdx.x;
+      if (i < i1) v[u] = *(const P3 *)(S.p + 3 * (size_t)i);
+    }
+#pragma unroll
+    for (int u = 0; u < kBinUnroll; ++u) {
+      const int i = ib + u * bd + (int)threadIdx.x;
+      if (i < i1) f(i, v[u], cell_of(&v[u].x, G));
+    }
+  }
+}
+
 __global__ __launch_bounds__(256) void k_bin_hist(BinJob J,
                                                   const GridParams *__restrict__ gp,
                                                   int *__restrict__ table) {
@@ -1113,9 +1140,7 @@ __global__ __launch_bounds__(256) void k_bin_hist(BinJob J,
   const GridParams G = *gp;
   for (int b = threadIdx.x; b < J.nb; b += blockDim.x) hist[b] = 0;
   __syncthreads();
-  const int i1 = min(S.n, (blk + 1) * S.P);
-  for (int i = blk * S.P + threadIdx.x; i < i1; i += blockDim.x)
-    atomicAdd(&hist[cell_of(S.p + 3 * (size_t)i, G) >> J.shift], 1);
+  bin_chunk(S, blk, G, [&](int, const P3 &, int c) { atomicAdd(&hist[c >> J.shift], 1); });
   __syncthreads();
   for (int b = threadIdx.x; b < J.nb; b += blockDim.x)
     table[S.tab + b * S.nblk + blk] = hist[b];
@@ -1133,23 +1158,20 @@ __global__ __launch_bounds__(256) void k_bin_scatter(BinJob J,
   for (int b = threadIdx.x; b < J.nb; b += blockDim.x)
     cur[b] = offs[S.tab + b * S.nblk + blk] - S.sub;
   __syncthreads();
-  const int i1 = min(S.n, (blk + 1) * S.P);
-  for (int i = blk * S.P + threadIdx.x; i < i1; i += blockDim.x) {
-    const double *pp = S.p + 3 * (size_t)i;
-    const int c = cell_of(pp, G);
+  bin_chunk(S, blk, G, [&](int i, const P3 &v, int c) {
     const int pos = atomicAdd(&cur[c >> J.shift], 1);
     if (side == 0) {
       BinPt t;
-      t.x = pp[0];
-      t.y = pp[1];
-      t.z = pp[2];
+      t.x = v.x;
+      t.y = v.y;
+      t.z = v.z;
       t.idx = i;
       t.cell = c;
       J.bin_t[pos] = t;
     } else {
       J.bin_q[pos] = make_int2(i, c);
     }
-  }
+  });
 }
 
 #ifndef NAVGPU_BIN_FINE_THREADS
@@ -1350,6 +1372,20 @@ struct RecPairCursor {  // global Rec16 array (two records of padding at its end
   __device__ void next() { p += 2; }
 };
 
+// key = (f32 distance bits with the low kKeyBits cleared) | local id, as ONE
+// v_and_or_b32 (the mask held in a VGPR, the id in an SGPR: the compiler
+// otherwise emits and + or / or3). lid MUST be wave-uniform: a divergent
+// value would be read from the first lane only.
+__device__ __forceinline__ uint32_t knn_key(float d, uint32_t vmask, uint32_t lid) {
+#ifdef NAVGPU_NO_ASM_KEY
+  return (__float_as_uint(d) & vmask) | lid;
+#else
+  uint32_t k;
+  asm("v_and_or_b32 %0, %1, %2, %3" : "=v"(k) : "v"(__float_as_uint(d)), "v"(vmask), "s"(lid));
+  return k;
+#endif
+}
+
 template <int K, class Runs, class CurF, class IdxF>
 __device__ __forceinline__ void knn_one(
     const GridParams &G, const double *__restrict__ tsort, const double qv[3],
@@ -1381,6 +1417,7 @@ __device__ __forceinline__ void knn_one(
     key[0] = min(key[0], kk);
   };
   constexpr uint32_t kOffMask = (1u << kRunOffBits) - 1;
+  const uint32_t vmask = ~kKeyMask;
 #pragma unroll 1
   for (int r = 0; r < 9; ++r) {
     int t0, t1, g0;
@@ -1392,8 +1429,8 @@ __device__ __forceinline__ void knn_one(
     auto cur = cursor(ta);
     if (np > 0) {  // first pair: may start before the run (odd t0) or end past it
       const f2 d = dist2(cur.load());
-      uint32_t k0 = (__float_as_uint(d[0]) & ~kKeyMask) | rid;
-      uint32_t k1 = (__float_as_uint(d[1]) & ~kKeyMask) | (rid + 1);
+      uint32_t k0 = knn_key(d[0], vmask, rid);
+      uint32_t k1 = knn_key(d[1], vmask, rid + 1);
       if (ta < t0) k0 = kNoKey;
       if (ta + 1 >= t1) k1 = kNoKey;
       ins(k0);
@@ -1402,20 +1439,31 @@ __device__ __forceinline__ void knn_one(
     }
     // interior pairs: both records inside the run, no masks; the key's local
     // id is the wave-uniform pair counter
+    // exit on the per-lane cursor reaching the last pair (one compare on the
+    // address the loop advances anyway, no separate per-lane trip counter).
+    // Only entered with np >= 3, so `last` lies past `cur`: LDS addresses
+    // start at 0, and a cursor before the run's start would wrap around.
+    if (np > 2) {
+      const auto last = cursor(ta + 2 * (np - 1));
+      uint32_t v2 = 2;
 #pragma unroll 1
-    for (int v = 1; v < np - 1; ++v) {
-      const f2 d = dist2(cur.load());
-      const uint32_t lid = rid | ((uint32_t)(2 * v) & kOffMask);
-      ins((__float_as_uint(d[0]) & ~kKeyMask) | lid);
-      ins((__float_as_uint(d[1]) & ~kKeyMask) | (lid + 1));
-      cur.next();
+      do {
+        const f2 d = dist2(cur.load());
+        const uint32_t lid = rid | (v2 & kOffMask);
+        ins(knn_key(d[0], vmask, lid));
+        ins(knn_key(d[1], vmask, lid + 1));
+        cur.next();
+        v2 += 2;
+      } while (cur.p < last.p);
     }
     if (np > 1) {  // last pair: may end past the run
       const f2 d = dist2(cur.load());
       const uint32_t lid = rid | ((uint32_t)(2 * (np - 1)) & kOffMask);
-      uint32_t k1 = (__float_as_uint(d[1]) & ~kKeyMask) | (lid + 1);
+      // lid depends on the lane's np here: divergent, so the plain and + or
+      // (knn_key wants a wave-uniform id in an SGPR)
+      uint32_t k1 = (__float_as_uint(d[1]) & vmask) | (lid + 1);
       if (ta + 2 * (np - 1) + 1 >= t1) k1 = kNoKey;
-      ins((__float_as_uint(d[0]) & ~kKeyMask) | lid);
+      ins((__float_as_uint(d[0]) & vmask) | lid);
       ins(k1);
     }
   }
@@ -1454,10 +1502,12 @@ __device__ __forceinline__ void knn_one(
     for (int s = 0; s < KL; ++s) {
       const bool v = key[s] != kNoKey;
       const int l = (int)((v ? key[s] : key[0]) & kKeyMask);
-      const int r = l >> kRunOffBits, off = l & ((1 << kRunOffBits) - 1);
+      const int r = min(l >> kRunOffBits, 8), off = l & ((1 << kRunOffBits) - 1);
       int t0, t1, g0;
       runs(r, t0, t1, g0);
-      const int p = (t0 & ~1) + off;  // record, in the fetch index space
+      // record, in the fetch index space; clamped into the run so that a
+      // corrupt id can never address outside the staged/sorted arrays
+      const int p = min(max((t0 & ~1) + off, t0), max(t1 - 1, t0));
       ei[s] = v ? fidx(p) : -1;
       gpos[s] = g0 + (p - t0);
     }
@@ -1515,11 +1565,22 @@ __device__ __forceinline__ void knn_one(
   ok = true;  // timing-only ablation builds: never take the slow path
 #endif
   if (ok) {
+#ifdef NAVGPU_DBG_NOOUT  // timing-only ablation: one store per query, data kept live
+    double acc = 0.0;
+    int iacc = 0;
+#pragma unroll
+    for (int s = 0; s < K; ++s) {
+      acc += ed[s];
+      iacc ^= ei[s];
+    }
+    oidx[q * K] = iacc + (int)acc;
+#else
 #pragma unroll
     for (int s = 0; s < K; ++s) {
       oidx[q * K + s] = ei[s];
       odist[q * K + s] = ed[s];
     }
+#endif
   } else {
     // K listed points have dsq <= dk2: a valid starting bound for the slow
     // path, which runs in its own launch (k_knn_slow)
@@ -1687,6 +1748,9 @@ __global__ __launch_bounds__(kTileThreads, NAVGPU_KNN_MINW) NAVGPU_KNN_ATTR void
     NV_STAMP_ADD(6, 0ull, 1ull);
     const int cell0 = (z * G.g[1] + y) * G.g[0];
     const int q0 = qstart[cell0 + xa], q1 = qstart[cell0 + xb + 1];
+#ifdef NAVGPU_DBG_NOQUERY  // timing-only ablation: staging and barriers only
+    if (q1 < 0)
+#endif
     for (int qi = q0 + threadIdx.x; qi < q1; qi += blockDim.x) {
       const size_t q = (size_t)qperm[qi];
       const double qv[3] = {qs[3 * q], qs[3 * q + 1], qs[3 * q + 2]};
@@ -2657,8 +2721,6 @@ static int knn_run(navgpu_ctx *ctx, const double *tgt, size_t nt, const double *
     const int ntabi = (int)ntab;
     hipLaunchKernelGGL(k_scan_sums, dim3(nbs), dim3(kScanBlock), 0, s, tab, ntabi, bsum);
     CHECK_LAUNCH("k_scan_sums");
-    hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(kScanBlock), 0, s, bsum, nbs);
-    CHECK_LAUNCH("k_scan_top");
     hipLaunchKernelGGL(k_scan_apply, dim3(nbs), dim3(kScanBlock), 0, s, tab, ntabi, bsum,
                        offs);
     CHECK_LAUNCH("k_scan_apply");
