@@ -11,9 +11,11 @@ front end on that pair, inputs already resident in HBM:
 value = matches (query points matched) over all ranks / max-over-ranks time.
 
 `--workload k2` runs the per-row slam.c mode instead (128x2048 L9-shaped
-pair, 1-NN, exact reference KD semantics) and `--workload k4` a batch of
+pair, 1-NN, exact reference KD semantics), `--workload k4` a batch of
 256 K2 pairs sharded over the ranks with an RCCL all-gather of the match
-sets (the north star's batched case).
+sets (the north star's batched case), and `--workload k5` the streaming
+L9 loop of src/main.c:361-431 (slam_localization + slam_mapping per frame)
+through the drop-in C ABI (libnavslam_128x2048.so), one step = one frame.
 
 Launch: python bench.py [--gpus N --steps K --warmup W]; for N > 1 under
 torch.distributed.run (one rank per GPU, RCCL).
@@ -39,7 +41,11 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=3)
-    p.add_argument("--workload", choices=["k3", "k2", "k4"], default="k3")
+    p.add_argument("--workload", choices=["k3", "k2", "k4", "k5"], default="k3")
+    p.add_argument("--stream-frames", type=int, default=8,
+                   help="k5: distinct ray-cast frames, replayed back and forth")
+    p.add_argument("--cpu-frames", type=int, default=3,
+                   help="k5: frames of the CPU reference run (pose RMSE + timing)")
     p.add_argument("--k", type=int, default=8)
     p.add_argument("--rows", type=int, default=None)
     p.add_argument("--cols", type=int, default=None)
@@ -153,9 +159,166 @@ def cpu_baseline_k2(src, tgt, reps):
                        "nearestNeighborSearch per source feature")}
 
 
+def run_k5(a, ws, rank, dev):
+    """K5 (BASELINE.json configs[4]): the L9 streaming loop of
+    src/main.c:361-431 through the drop-in ABI -- init_slam on frame 0, then per
+    frame slam_localization(frame, last, last) + slam_mapping(measured). Every
+    frame rebuilds the target (per-row trees of the new frame's features in
+    the global frame) on the GPU; dedup and the 3-DOF Adam run on the host,
+    bit-exact (their sequential f64 sums fix the rounding order). Host
+    pointers in and out, as the reference API has them: the per-frame PCIe
+    copies are inside the timed region. Replicas only (a pose chain does not
+    shard): each rank runs its own stream."""
+    import torch
+    import torch.distributed as dist
+    from navslam import shard, synth
+    from navslam.abi import Pos, Shim
+    os.environ.setdefault("NAVSLAM_QUIET", "1")   # no per-iteration printf
+    os.environ.setdefault("NAVSLAM_DEVICE", str(dev.index))
+    R, Cc = a.rows or 128, a.cols or 2048
+    F = max(1, a.stream_frames)
+    frames = synth.l9_stream(R, Cc, F, seed=11 + rank)
+    sh = Shim(R, Cc)
+    pcs = [sh.cloud(frames[f], ts=f) for f in range(F)]
+    attr = sh.SLAMAttr()
+    zero = Pos.of([0.0] * 6)
+    sh.L.init_slam(attr, zero, pcs[0])
+    poses, state = [], {"i": 0, "last": zero, "q": 0}
+
+    def frame():
+        state["i"] += 1
+        pc = pcs[synth.l9_stream_index(state["i"], F)]
+        last = state["last"]
+        meas = sh.L.slam_localization(attr, pc, last, last)
+        sh.L.slam_mapping(attr, meas, pc)
+        state["last"] = meas
+        state["q"] += sh.last_frame_stats()[0]
+        poses.append(meas.tolist())
+
+    for _ in range(a.warmup):
+        frame()
+    torch.cuda.synchronize()
+    if ws > 1:
+        dist.barrier()
+    ctx = sh.context()
+    from navslam.gpu import load_library
+    L = load_library()
+    L.navgpu_timing_enable(ctx, 1)
+    names = ["rows_build", "rows_query"]
+    for n in names:
+        L.navgpu_timing_read(ctx, n.encode(), 1)
+    q0 = state["q"]
+    torch.cuda.synchronize()
+    if ws > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        frame()
+    torch.cuda.synchronize()
+    if ws > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
+    L.navgpu_timing_enable(ctx, 0)
+    kt = {}
+    for n in names:
+        cnt = L.navgpu_timing_count(ctx, n.encode())
+        kt[n] = (L.navgpu_timing_read(ctx, n.encode(), 1), cnt)
+    elapsed = shard.max_over_ranks(t1 - t0, dev)
+    matches = shard.sum_over_ranks(state["q"] - q0, dev)
+    frames_all = shard.sum_over_ranks(a.steps, dev)
+    if rank != 0:
+        return None
+    cpu = None
+    if not a.no_cpu_baseline and a.cpu_frames > 0:
+        cpu = cpu_baseline_k5(frames, F, min(a.cpu_frames, len(poses)), poses)
+    per_frame = lambda n: 1000.0 * kt[n][0] / max(kt[n][1], 1)
+    gpu_us = sum(per_frame(n) for n in names)
+    # SURVEY 8(d) bytes per frame, per-row mode: build reads 24 B per target
+    # feature point + the query stage 24 B per query + 24 B per target
+    # feature + 12 B per match (k = 1): with T ~ Q ~ queries per frame
+    qpf = (state["q"] - q0) / max(a.steps, 1)
+    bytes_pf = int(24 * qpf + (24 + 24 + 12) * qpf)
+    ach = bytes_pf / (gpu_us * 1e-6) / 1e9 if gpu_us > 0 else None
+    roof = {"bound": "hbm", "achieved": round(ach, 2) if ach else None, "peak": HBM_PEAK_GBS,
+            "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 6) if ach else None,
+            "traffic": None, "kernel": "k_rows_build + k_rows_query per frame",
+            "avg_us": round(gpu_us, 2), "bytes_per_launch": bytes_pf,
+            "bytes_model": "24 B/target feature (build) + 24 Q + 24 T + 12 Q (query), SURVEY 8d",
+            "note": "latency-bound per-row kernels; a frame is host-bound (sequential Adam)"}
+    out = {"metric": METRIC, "value": round(matches / elapsed, 1), "unit": "matches/s",
+           "n_gpus": ws, "steps": a.steps, "warmup": a.warmup,
+           "ms_per_step": round(1000.0 * elapsed / a.steps, 4), "higher_is_better": True,
+           "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+           "data": (f"synthetic L9 stream: {F} ray-cast {R}x{Cc} frames along a walk "
+                    "(navslam.synth.l9_stream), replayed back and forth"),
+           "config": {"workload": (f"K5: streaming L9 loop (src/main.c:361-431) through the "
+                                   f"drop-in ABI, {R}x{Cc} frames, per-frame target rebuild, "
+                                   "bit-exact host dedup + Adam"),
+                      "parallelism": f"replicas x{ws}", "points_per_frame": R * Cc,
+                      "frames_per_s": round(frames_all / elapsed, 2),
+                      "queries_per_frame": round(qpf, 1), "mode": "rows"},
+           "roofline": roof, "curvature_plus_query": None,
+           "kernel_us": {n: round(per_frame(n), 2) for n in names},
+           "cpu_baseline": cpu}
+    return out
+
+
+def cpu_baseline_k5(frames, F, nf, gpu_poses):
+    """The same stream's first `nf` frames through the oracle's restatement of
+    src/slam.c (single-threaded; the reference's own build is fixed to 8x8,
+    utils/pointcloud.h:9-10): seconds per frame, and the pose RMSE of the
+    GPU run against it over those frames."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    from pyoracle import Oracle, OracleSlam
+    from navslam import synth
+    orc = Oracle()
+    R, Cc = frames.shape[1], frames.shape[2]
+    s = OracleSlam(orc, R, Cc)
+    z = np.zeros(6)
+    s.init(z, frames[0])
+    last, poses, ts = z, [], []
+    for i in range(1, nf + 1):
+        f = frames[synth.l9_stream_index(i, F)]
+        t0 = time.perf_counter()
+        meas, _, _ = s.localization(f, last, last)
+        s.mapping(meas, f)
+        ts.append(time.perf_counter() - t0)
+        poses.append(meas)
+        last = meas
+    g = np.asarray(gpu_poses[:nf])[:, :3]
+    c = np.asarray(poses)[:, :3]
+    rmse = float(np.sqrt(np.mean(np.sum((g - c) ** 2, axis=1))))
+    exact = bool(np.array_equal(np.asarray(gpu_poses[:nf]), np.asarray(poses)))
+    t = float(np.median(ts))
+    return {"value": None, "unit": "s/frame", "seconds_per_frame": t,
+            "frames_per_s": 1.0 / t, "cores": 1, "kind": "port",
+            "pose_rmse_mm": rmse, "pose_bit_exact": exact,
+            "sample": (f"the first {nf} frames of the same stream through the oracle's "
+                       "restatement of src/slam.c at this grid (pinned bit-exact to the "
+                       "reference build by tests/golden), median frame time")}
+
+
 def main():
     a = parse()
     ws, rank, local = dist_env()
+    if a.workload == "k5":
+        import torch
+        import torch.distributed as dist
+        if ws > 1:
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        dev = torch.device("cuda", local if ws > 1 else 0)
+        torch.cuda.set_device(dev)
+        out = run_k5(a, ws, rank, dev)
+        if out is not None:
+            line = json.dumps(out)
+            print(line, flush=True)
+            if a.json_out:
+                with open(a.json_out, "w") as f:
+                    f.write(line + "\n")
+        if ws > 1:
+            dist.destroy_process_group()
+        return out
     import torch
     import torch.distributed as dist
     if ws > 1:

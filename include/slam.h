@@ -38,4 +38,15 @@ Pos slam_localization(SLAM_attr *attr, PointCloud *lidarPointCloud, Pos pos_pred
 /* headers/slam.h:28 / src/slam.c:393-431 */
 void slam_mapping(SLAM_attr *attr, Pos pos, PointCloud *lidarPointCloud);
 
+/* Extensions (not in the reference; a harness may ignore them) --------- */
+
+/* The navgpu_ctx* the library runs on (include/navgpu.h), e.g. to switch
+ * kernel timing on with navgpu_timing(). */
+void *navslam_context(void);
+
+/* Counts of the last slam_localization call: feature queries searched,
+ * correspondences kept by the dedup (CPcount, src/slam.c:284), Adam
+ * iterations run (src/slam.c:300-379). Returns 0. */
+int navslam_last_frame_stats(int *queries, int *correspondences, int *iterations);
+
 #endif

@@ -223,7 +223,37 @@ void extract_feature(PointCloud *lidarPointCloud,
                 feature[i][j] = 1;
 }
 
+/* ------------------------------------------ extras (not in the reference) */
+static int g_last_queries, g_last_cp, g_last_iters;
+
+/* The navgpu context the shim runs on, so a host harness can switch its
+ * kernel timing on (navgpu_timing / navgpu_timing_read). */
+void *navslam_context(void)
+{
+    return ctx();
+}
+
+/* Counts of the last slam_localization call: feature queries searched,
+ * correspondences after the dedup (CPcount, src/slam.c:284) and Adam
+ * iterations run (src/slam.c:300-379). Returns 0. */
+int navslam_last_frame_stats(int *queries, int *correspondences, int *iterations)
+{
+    if (queries)
+        *queries = g_last_queries;
+    if (correspondences)
+        *correspondences = g_last_cp;
+    if (iterations)
+        *iterations = g_last_iters;
+    return 0;
+}
+
 /* ------------------------------------------------ SLAM_attr side table */
+/* dedup hash slot: a nearest point's coordinates -> its correspondence */
+typedef struct {
+    double key[3];
+    int32_t idx;
+} dedup_slot;
+
 typedef struct {
     SLAM_attr *key;
     double *d_lidar, *d_global, *d_last, *d_tree, *d_dist;
@@ -236,6 +266,9 @@ typedef struct {
     double h_tp[NPTS * 3];
     double h_dist[NPTS];
     int32_t h_pos[NPTS];
+    NeighborResult *result; /* correspondence list (src/slam.c:214) */
+    dedup_slot *tab;
+    int32_t *used;
 } slam_state;
 
 static slam_state **g_states;
@@ -332,11 +365,6 @@ void slam_mapping(SLAM_attr *attr, Pos pos, PointCloud *lidarPointCloud)
     attr->frameCount++;
 }
 
-/* correspondence list entry: NeighborResult (utils/kdtree.h:14-18) */
-typedef struct {
-    double key[3];
-    int32_t idx;
-} dedup_slot;
 
 static uint64_t key_bits(double v)
 {
@@ -388,19 +416,26 @@ Pos slam_localization(SLAM_attr *attr, PointCloud *lidarPointCloud,
     CK(navgpu_sync(c));
 
     /* host: dedup (src/slam.c:235-284) */
-    NeighborResult *result = malloc(sizeof(NeighborResult) * (NPTS ? NPTS : 1));
+    /* per-state scratch, allocated once (a fresh 56 B x R*C list every frame
+     * costs its page faults again) */
     size_t tcap = 16;
     while (tcap < 2 * (size_t)COLS)
         tcap <<= 1;
-    dedup_slot *tab = malloc(sizeof(dedup_slot) * tcap);
-    int32_t *used = malloc(sizeof(int32_t) * tcap);
-    if (!result || !tab || !used) {
-        fprintf(stderr, "navslam: out of host memory\n");
-        abort();
+    if (!s->result) {
+        s->result = malloc(sizeof(NeighborResult) * (NPTS ? NPTS : 1));
+        s->tab = malloc(sizeof(dedup_slot) * tcap);
+        s->used = malloc(sizeof(int32_t) * tcap);
+        if (!s->result || !s->tab || !s->used) {
+            fprintf(stderr, "navslam: out of host memory\n");
+            abort();
+        }
     }
+    NeighborResult *result = s->result;
+    dedup_slot *tab = s->tab;
+    int32_t *used = s->used;
     for (size_t i = 0; i < tcap; i++)
         tab[i].idx = -1;
-    int CPcount = 0;
+    int CPcount = 0, nqueries = 0;
     for (int row = 0; row < ROWS; ++row) {
         int nused = 0;
         const double *tree = s->h_tree + 3 * (size_t)row * COLS;
@@ -412,6 +447,7 @@ Pos slam_localization(SLAM_attr *attr, PointCloud *lidarPointCloud,
              * no correspondence */
             if (pos < 0)
                 continue;
+            nqueries++;
             const double *np = tree + 3 * (size_t)pos;
             double bestDist = s->h_dist[g];
             int nan = np[0] != np[0] || np[1] != np[1] || np[2] != np[2];
@@ -448,8 +484,6 @@ Pos slam_localization(SLAM_attr *attr, PointCloud *lidarPointCloud,
         for (int i = 0; i < nused; i++)
             tab[used[i]].idx = -1;
     }
-    free(tab);
-    free(used);
 
     /* host: Adam on the translation (src/slam.c:218-379) */
     double learningRate = 0.1, tolerance = 1e-6;
@@ -458,7 +492,8 @@ Pos slam_localization(SLAM_attr *attr, PointCloud *lidarPointCloud,
     double m[3] = {0.0, 0.0, 0.0}, v[3] = {0.0, 0.0, 0.0};
     double beta1 = 0.9, beta2 = 0.999, epsilon = 1e-8;
     int q = quiet();
-    for (int iter = 0; iter < 200; ++iter) {
+    int iter;
+    for (iter = 0; iter < 200; ++iter) {
         double gradient[3] = {0.0, 0.0, 0.0};
         totalError = 0;
         validGradientCount = 0;
@@ -496,7 +531,9 @@ Pos slam_localization(SLAM_attr *attr, PointCloud *lidarPointCloud,
         if (!q)
             printf("Iteration %d, Total Error: %.6f\n", iter, totalError);
     }
-    free(result);
+    g_last_queries = nqueries;
+    g_last_cp = CPcount;
+    g_last_iters = iter; /* the iteration that converged, or 200 */
     if (validGradientCount > 0)
         attr->error = sqrt(totalError / validGradientCount);
     else

@@ -111,3 +111,30 @@ def l5_stream(rng, frames, R=8, C=8):
         d = d + rng.integers(-4, 5, (R, C))
         depth[f] = np.round(d).astype(np.int32)
     return depth, imu
+
+
+def l9_stream(R=128, C=2048, frames=8, seed=11, step=(40.0, 15.0, 0.0), yaw_step_deg=0.25,
+              integer_mm=False):
+    """K5: sensor-frame L9-shaped scans [F, R, C, 3] along a straight walk
+    through the room (``step`` mm and ``yaw_step_deg`` per frame), the input
+    of the src/main.c:361-431 L9 loop. Ray-casting costs ~0.4 s per
+    128x2048 frame, so long streams replay these frames back and forth
+    (``l9_stream_index``)."""
+    rng = np.random.default_rng(seed)
+    out = np.empty((frames, R, C, 3))
+    for f in range(frames):
+        origin = (step[0] * f, step[1] * f, step[2] * f)
+        out[f] = _scan(R, C, origin, yaw_step_deg * f, rng)
+    if integer_mm:
+        out = np.round(out)
+    return out
+
+
+def l9_stream_index(i, frames):
+    """Frame of a ping-pong replay 0, 1, ..., F-1, F-2, ..., 1, 0, 1, ... so a
+    long stream keeps moving continuously."""
+    if frames <= 1:
+        return 0
+    p = 2 * (frames - 1)
+    j = i % p
+    return j if j < frames else p - j

@@ -386,6 +386,41 @@ def test_shim_stream_vs_oracle(monkeypatch, R, Cc, frames):
     _eq(got["last_global"], s.last_global(), "last global frame")
 
 
+@pytest.mark.parametrize("R,Cc,F,steps", [(54, 42, 4, 9), (128, 2048, 3, 4)])
+def test_shim_l9_stream_vs_oracle(monkeypatch, R, Cc, F, steps):
+    """K5 shape: the L9 loop of src/main.c:423-431 (localization with
+    pred = last, then mapping at the measured pose) over a ray-cast stream
+    replayed back and forth, through the drop-in ABI; every pose, error and
+    the frame stats bit-exact against the oracle's slam.c restatement."""
+    monkeypatch.setenv("NAVSLAM_QUIET", "1")
+    from pyoracle import Oracle, OracleSlam
+    from shimlib import Pos, Shim
+    from navslam.synth import l9_stream, l9_stream_index
+    frames = l9_stream(R, Cc, F, seed=17)
+    sh = Shim(R, Cc)
+    attr = sh.SLAMAttr()
+    pcs = [sh.cloud(f) for f in frames]
+    zero = np.zeros(6)
+    sh.L.init_slam(C.byref(attr), Pos.of(zero), C.byref(pcs[0]))
+    orc = Oracle()
+    s = OracleSlam(orc, R, Cc)
+    s.init(zero, frames[0])
+    last_g, last_o = Pos.of(zero), zero
+    for i in range(1, steps + 1):
+        f = l9_stream_index(i, F)
+        meas = sh.L.slam_localization(C.byref(attr), C.byref(pcs[f]), last_g, last_g)
+        sh.L.slam_mapping(C.byref(attr), meas, C.byref(pcs[f]))
+        om, iters, ncp = s.localization(frames[f], last_o, last_o)
+        s.mapping(om, frames[f])
+        _eq(np.array(meas.tolist()), om, f"frame {i} pose")
+        assert attr.error == s.error, f"frame {i} error"
+        q, cp, it = sh.last_frame_stats()
+        assert (cp, it) == (ncp, iters), f"frame {i} stats {(cp, it)} vs {(ncp, iters)}"
+        assert q >= cp
+        last_g, last_o = meas, om
+    assert attr.frameCount == s.frame_count
+
+
 def test_shim_kdtree_api_matches_reference_golden(golden):
     from shimlib import KDNode, Point, Shim, preorder
     sh = Shim(8, 8)
