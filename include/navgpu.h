@@ -114,6 +114,20 @@ int navgpu_kd_query_rows_dev(navgpu_ctx *ctx, const double *tree_pts,
                              int32_t *nn_pos, double *nn_dist,
                              int32_t *mask_out);
 
+/* ---- R7: correspondence dedup per row (src/slam.c:247-284) -------------
+ * Over the output of navgpu_kd_query_rows: of the queries of row r whose
+ * nearest points have equal coordinates, keep the first column at the
+ * smallest distance (the reference list's final entry). keep[r*C+c] = 1 for
+ * a kept correspondence (nullable); sums[r*6 .. r*6+4] = sum over kept
+ * pairs of d = ori - nearest: d.x, d.y, d.z, |d|^2, count; sums[r*6+5] =
+ * the row's queries that found a nearest point. Order-free: used
+ * by the shim's closed-form Adam (NAVSLAM_ADAM=fast); the bit-exact mode
+ * keeps the reference's sequential list on the host. */
+int navgpu_rows_corr_dev(navgpu_ctx *ctx, const double *tree_pts,
+                         const int32_t *tree_n, const int32_t *nn_pos,
+                         const double *nn_dist, const double *ori, int R, int C,
+                         int32_t *keep, double *sums);
+
 /* ---- The K2 scan-pair step, per-row mode (fused, one kernel) ------------
  * masks of src and tgt (R1), per-row target trees (R4+R5), every src
  * feature queried against its row's tree (R6). nn_idx = linear target index

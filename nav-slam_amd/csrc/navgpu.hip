@@ -834,6 +834,120 @@ inline int kd_build_lds_bytes(int n) {
   return align16(24 * n) + 2 * align16(2 * n);
 }
 
+// ------------------------------------------------- R7: correspondence dedup
+// src/slam.c:247-284, one workgroup per row: of the row's feature queries
+// that found the same nearest point (coordinate equality, -0.0 == 0.0), the
+// kept one is the first (lowest column) at the smallest distance -- what the
+// reference's "replace only if strictly closer" list update leaves. Nearest
+// points are canonicalised through an LDS hash of the row tree's
+// coordinates (first-come owner per distinct coordinate triple), the
+// per-point minimum is two LDS atomicMin passes (distance bits, then
+// column). Outputs: keep[r*C+c] (1 = kept correspondence; nullable) and the
+// row's residual sums over kept pairs, d = ori - near:
+//   sums[r*6 + {0,1,2}] = sum d.x, d.y, d.z; [3] = sum |d|^2; [4] = count;
+//   [5] = queries of the row that found a nearest point (before the dedup).
+// Order-free: the sums are what a closed-form Adam step needs (the
+// reference's own sequential sum order is kept by the host path instead).
+// A nearest point with a NaN coordinate never matches another (== is false)
+// and stays its own correspondence, as in the reference.
+constexpr int kCorrBlock = 512;
+
+__device__ __forceinline__ uint64_t corr_key_bits(double v) {
+  return (uint64_t)__double_as_longlong(v == 0.0 ? 0.0 : v);
+}
+
+__global__ __launch_bounds__(kCorrBlock) void k_rows_corr(
+    const double *__restrict__ tree_pts, const int32_t *__restrict__ tree_n,
+    const int32_t *__restrict__ nn_pos, const double *__restrict__ nn_dist,
+    const double *__restrict__ ori, int C, int HS, int32_t *__restrict__ keep,
+    double *__restrict__ sums) {
+  extern __shared__ __attribute__((aligned(8))) unsigned char corr_lds[];
+  unsigned long long *bdist = (unsigned long long *)corr_lds;  // [HS]
+  int *owner = (int *)(bdist + HS);                            // [HS]
+  int *bcol = owner + HS;                                      // [HS]
+  int *canon = bcol + HS;                                      // [C]
+  __shared__ double red[kCorrBlock / kWave][6];
+  const int row = blockIdx.x;
+  const size_t base = (size_t)row * C;
+  const int n = tree_n[row];
+  for (int h = threadIdx.x; h < HS; h += blockDim.x) {
+    owner[h] = -1;
+    bdist[h] = ~0ull;
+    bcol[h] = INT_MAX;
+  }
+  __syncthreads();
+  // canonical slot of every tree point (-1: a NaN coordinate)
+  for (int p = threadIdx.x; p < n; p += blockDim.x) {
+    const double *tp = tree_pts + 3 * (base + p);
+    const double x = tp[0], y = tp[1], z = tp[2];
+    if (x != x || y != y || z != z) {
+      canon[p] = -1;
+      continue;
+    }
+    uint64_t hh = corr_key_bits(x) * 0x9E3779B97F4A7C15ull;
+    hh ^= corr_key_bits(y) + 0x632BE59BD9B4E019ull + (hh << 6) + (hh >> 2);
+    hh ^= corr_key_bits(z) + 0x85EBCA77C2B2AE63ull + (hh << 6) + (hh >> 2);
+    int h = (int)((hh ^ (hh >> 29)) & (uint64_t)(HS - 1));
+    // HS >= 2C > n: the probe always finds a free or matching slot
+    for (;;) {
+      const int o = atomicCAS(&owner[h], -1, p);
+      if (o < 0) break;
+      const double *op = tree_pts + 3 * (base + o);
+      if (op[0] == x && op[1] == y && op[2] == z) break;
+      h = (h + 1) & (HS - 1);
+    }
+    canon[p] = h;
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+    const int pos = nn_pos[base + c];
+    if (pos < 0 || pos >= n) continue;
+    const int h = canon[pos];
+    if (h >= 0) atomicMin(&bdist[h], (unsigned long long)__double_as_longlong(nn_dist[base + c]));
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+    const int pos = nn_pos[base + c];
+    if (pos < 0 || pos >= n) continue;
+    const int h = canon[pos];
+    if (h >= 0 && (unsigned long long)__double_as_longlong(nn_dist[base + c]) == bdist[h])
+      atomicMin(&bcol[h], c);
+  }
+  __syncthreads();
+  double acc[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+    const int pos = nn_pos[base + c];
+    bool kept = false;
+    if (pos >= 0 && pos < n) {
+      const int h = canon[pos];
+      kept = h < 0 || bcol[h] == c;
+      acc[5] += 1.0;
+    }
+    if (keep) keep[base + c] = kept ? 1 : 0;
+    if (kept) {
+      const double *a = ori + 3 * (base + c), *b = tree_pts + 3 * (base + pos);
+      const double dx = a[0] - b[0], dy = a[1] - b[1], dz = a[2] - b[2];
+      acc[0] += dx;
+      acc[1] += dy;
+      acc[2] += dz;
+      acc[3] += dx * dx + dy * dy + dz * dz;
+      acc[4] += 1.0;
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 6; ++k)
+    for (int o = kWave / 2; o > 0; o >>= 1) acc[k] += __shfl_xor(acc[k], o, kWave);
+  if ((threadIdx.x & (kWave - 1)) == 0)
+#pragma unroll
+    for (int k = 0; k < 6; ++k) red[threadIdx.x / kWave][k] = acc[k];
+  __syncthreads();
+  if (threadIdx.x < 6) {
+    double t = 0.0;
+    for (int w = 0; w < kCorrBlock / kWave; ++w) t += red[w][threadIdx.x];
+    sums[(size_t)row * 6 + threadIdx.x] = t;
+  }
+}
+
 // ============================================================ global mode
 // Uniform grid over the target cloud. Cells are numbered x-fastest, so the
 // cells x-1..x+1 of one (y,z) row are contiguous in the cell-sorted target
@@ -2484,6 +2598,28 @@ int navgpu_kd_query_rows_dev(navgpu_ctx *ctx, const double *tree_pts,
                      ctx->stream, tree_pts, tree_n, feat_src, queries, R, C,
                      nn_pos, nn_dist, mask_out);
   CHECK_LAUNCH("k_rows_query");
+  return NAVGPU_OK;
+}
+
+int navgpu_rows_corr_dev(navgpu_ctx *ctx, const double *tree_pts,
+                         const int32_t *tree_n, const int32_t *nn_pos,
+                         const double *nn_dist, const double *ori, int R, int C,
+                         int32_t *keep, double *sums) {
+  ARG_CHECK(ctx && R >= 0 && C >= 0);
+  if (C > kMaxRowCols) {
+    set_err("rows_corr: C=%d exceeds %d", C, kMaxRowCols);
+    return NAVGPU_ERANGE;
+  }
+  if ((size_t)R * C == 0) return NAVGPU_OK;
+  ARG_CHECK(tree_pts && tree_n && nn_pos && nn_dist && ori && sums);
+  int HS = 64;
+  while (HS < 2 * C) HS <<= 1;
+  const int lds = HS * (8 + 4 + 4) + 4 * C;
+  RC(set_lds(k_rows_corr, lds));
+  TimedRegion tr(ctx, "rows_corr");
+  hipLaunchKernelGGL(k_rows_corr, dim3(R), dim3(kCorrBlock), lds, ctx->stream, tree_pts,
+                     tree_n, nn_pos, nn_dist, ori, C, HS, keep, sums);
+  CHECK_LAUNCH("k_rows_corr");
   return NAVGPU_OK;
 }
 

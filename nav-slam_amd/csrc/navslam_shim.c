@@ -69,6 +69,16 @@ static int quiet(void)
     return q && *q && *q != '0';
 }
 
+/* NAVSLAM_ADAM=fast: correspondence dedup on the GPU and the Adam loop on
+ * closed-form residual sums (order-free, so not bit-identical to the
+ * reference's sequential sums; the pose difference is reported by
+ * bench.py --workload k5 --k5-mode fast). Default: bit-exact host path. */
+static int adam_fast(void)
+{
+    const char *q = getenv("NAVSLAM_ADAM");
+    return q && strcmp(q, "fast") == 0;
+}
+
 static int host_trees(void)
 {
     const char *q = getenv("NAVSLAM_HOST_TREES");
@@ -256,7 +266,8 @@ typedef struct {
 
 typedef struct {
     SLAM_attr *key;
-    double *d_lidar, *d_global, *d_last, *d_tree, *d_dist;
+    double *d_lidar, *d_global, *d_last, *d_tree, *d_dist, *d_sums;
+    double h_sums[6 * ROWS];
     int32_t *d_tcol, *d_tn, *d_pos;
     int have_trees;
     double h_tree[NPTS * 3];
@@ -294,6 +305,7 @@ static slam_state *state_for(SLAM_attr *a)
     CK(navgpu_malloc(c, 4 * NPTS, (void **)&s->d_tcol));
     CK(navgpu_malloc(c, 4 * ROWS, (void **)&s->d_tn));
     CK(navgpu_malloc(c, 4 * NPTS, (void **)&s->d_pos));
+    CK(navgpu_malloc(c, 8 * 6 * ROWS, (void **)&s->d_sums));
     g_states = realloc(g_states, sizeof(*g_states) * (g_nstates + 1));
     g_states[g_nstates++] = s;
     return s;
@@ -383,6 +395,80 @@ static uint64_t hash3(const double *p)
     return h ^ (h >> 29);
 }
 
+/* The NAVSLAM_ADAM=fast tail of slam_localization: dedup + residual sums on
+ * the GPU (navgpu_rows_corr_dev), then src/slam.c:300-389's Adam loop with
+ * every per-iteration sum in closed form. With d_i = ori_i - near_i and
+ * dx_i = (ori_i - t) - near_i = d_i - t:
+ *   sum dx = S1 - n t,   totalError = sum |d_i - t|^2 = S2 - 2 t.S1 + n |t|^2
+ * (exact in real arithmetic; rounding differs from the sequential sums). */
+static Pos localization_fast(SLAM_attr *attr, slam_state *s, double transform[6],
+                             Pos pos_last)
+{
+    navgpu_ctx *c = ctx();
+    CK(navgpu_rows_corr_dev(c, s->d_tree, s->d_tn, s->d_pos, s->d_dist, s->d_global,
+                            ROWS, COLS, NULL, s->d_sums));
+    CK(navgpu_download(c, s->h_sums, s->d_sums, sizeof(s->h_sums)));
+    CK(navgpu_sync(c));
+    double S1[3] = {0.0, 0.0, 0.0}, S2 = 0.0, n = 0.0, nq = 0.0;
+    for (int r = 0; r < ROWS; r++) {
+        const double *h = s->h_sums + 6 * r;
+        S1[0] += h[0];
+        S1[1] += h[1];
+        S1[2] += h[2];
+        S2 += h[3];
+        n += h[4];
+        nq += h[5];
+    }
+    double learningRate = 0.1, tolerance = 1e-6;
+    double previousTotalError = 0, totalError = 0;
+    double m[3] = {0.0, 0.0, 0.0}, v[3] = {0.0, 0.0, 0.0};
+    double beta1 = 0.9, beta2 = 0.999, epsilon = 1e-8;
+    int q = quiet();
+    int iter;
+    for (iter = 0; iter < 200; ++iter) {
+        const double *t = transform;
+        double gradient[3];
+        for (int j = 0; j < 3; j++)
+            gradient[j] = -(S1[j] - n * t[j]);
+        totalError = S2 - 2.0 * (t[0] * S1[0] + t[1] * S1[1] + t[2] * S1[2]) +
+                     n * (t[0] * t[0] + t[1] * t[1] + t[2] * t[2]);
+        if (fabs(totalError - previousTotalError) < tolerance) {
+            if (!q)
+                printf("\xe6\x94\xb6\xe6\x95\x9b\xef\xbc\x8c\xe5\x81\x9c\xe6\xad\xa2"
+                       "\xe8\xbf\xad\xe4\xbb\xa3\xef\xbc\x81\n");
+            break;
+        }
+        previousTotalError = totalError;
+        if (n > 0) {
+            gradient[0] /= n;
+            gradient[1] /= n;
+            gradient[2] /= n;
+        }
+        int tt = iter + 1;
+        for (int j = 0; j < 3; j++) {
+            m[j] = beta1 * m[j] + (1 - beta1) * gradient[j];
+            v[j] = beta2 * v[j] + (1 - beta2) * gradient[j] * gradient[j];
+            double m_hat = m[j] / (1 - pow(beta1, tt));
+            double v_hat = v[j] / (1 - pow(beta2, tt));
+            transform[j] -= learningRate * m_hat / (sqrt(v_hat) + epsilon);
+        }
+        if (!q)
+            printf("Iteration %d, Total Error: %.6f\n", iter, totalError);
+    }
+    g_last_queries = (int)nq;
+    g_last_cp = (int)n;
+    g_last_iters = iter;
+    attr->error = n > 0 ? sqrt(totalError / n) : 0.0;
+    Pos out;
+    out.x = pos_last.x + transform[0];
+    out.y = pos_last.y + transform[1];
+    out.z = pos_last.z + transform[2];
+    out.roll = pos_last.roll + transform[3];
+    out.pitch = pos_last.pitch + transform[4];
+    out.yaw = pos_last.yaw + transform[5];
+    return out;
+}
+
 Pos slam_localization(SLAM_attr *attr, PointCloud *lidarPointCloud,
                       Pos pos_predict, Pos pos_last)
 {
@@ -410,6 +496,8 @@ Pos slam_localization(SLAM_attr *attr, PointCloud *lidarPointCloud,
     }
     CK(navgpu_kd_query_rows_dev(c, s->d_tree, s->d_tn, s->d_lidar, s->d_last,
                                 ROWS, COLS, s->d_pos, s->d_dist, NULL));
+    if (adam_fast())
+        return localization_fast(attr, s, transform, pos_last);
     CK(navgpu_download(c, s->h_pos, s->d_pos, 4 * NPTS));
     CK(navgpu_download(c, s->h_dist, s->d_dist, 8 * NPTS));
     CK(navgpu_download(c, s->h_tp, s->d_global, 24 * NPTS));

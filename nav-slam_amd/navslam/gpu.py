@@ -44,6 +44,8 @@ def _declare(L):
                                                _vp, _vp, _vp, _vp]),
         "navgpu_kd_query_rows_dev": (C.c_int, [_vp, _vp, _vp, _vp, _vp, C.c_int,
                                                C.c_int, _vp, _vp, _vp]),
+        "navgpu_rows_corr_dev": (C.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, C.c_int,
+                                           C.c_int, _vp, _vp]),
         "navgpu_rows_match_dev": (C.c_int, [_vp, _vp, _vp, C.c_int, C.c_int,
                                             _vp, _vp, _vp, _vp]),
         "navgpu_rows_match_host": (C.c_int, [_vp, _vp, _vp, C.c_int, C.c_int,
@@ -231,6 +233,11 @@ class NavGpu:
         self._check(self.L.navgpu_kd_query_rows_dev(
             self.h, _ptr(tree_pts), _ptr(tree_n), _ptr(feat_src), _ptr(queries), R, Cc,
             _ptr(nn_pos), _ptr(nn_dist), _ptr(mask)), "kd_query_rows_dev")
+
+    def rows_corr_dev(self, tree_pts, tree_n, nn_pos, nn_dist, ori, R, Cc, keep, sums):
+        self._check(self.L.navgpu_rows_corr_dev(
+            self.h, _ptr(tree_pts), _ptr(tree_n), _ptr(nn_pos), _ptr(nn_dist), _ptr(ori),
+            R, Cc, _ptr(keep), _ptr(sums)), "rows_corr")
 
     def rows_match_dev(self, src, tgt, R, Cc, src_mask, tgt_mask, nn_idx, nn_dist):
         self._check(self.L.navgpu_rows_match_dev(

@@ -421,6 +421,103 @@ def test_shim_l9_stream_vs_oracle(monkeypatch, R, Cc, F, steps):
     assert attr.frameCount == s.frame_count
 
 
+def _dedup_reference(tree, tn, pos, dist, ori):
+    """src/slam.c:247-284 per row, in Python: first-insertion list keyed on
+    nearest-point coordinate equality, replaced only by a strictly closer
+    query. Returns the keep mask and the per-row sums of d = ori - near."""
+    R, Cc = pos.shape
+    keep = np.zeros((R, Cc), np.int32)
+    sums = np.zeros((R, 6))
+    for r in range(R):
+        entries = {}
+        for c in range(Cc):
+            p = int(pos[r, c])
+            if p < 0:
+                continue
+            sums[r, 5] += 1
+            near = tree[r, p]
+            key = tuple(0.0 if v == 0 else float(v) for v in near)
+            if any(v != v for v in key):
+                entries[("nan", c)] = c
+                continue
+            if key in entries:
+                if dist[r, entries[key]] > dist[r, c]:
+                    entries[key] = c
+            else:
+                entries[key] = c
+        for c in entries.values():
+            keep[r, c] = 1
+            d = ori[r, c] - tree[r, int(pos[r, c])]
+            sums[r, :3] += d
+            sums[r, 3] += d @ d
+            sums[r, 4] += 1
+    return keep, sums
+
+
+@pytest.mark.parametrize("integer_mm", [False, True])
+def test_rows_corr_matches_reference_dedup(gpu, integer_mm):
+    """R7 on the GPU (navgpu_rows_corr_dev) against the reference list rule,
+    on real per-row trees/queries; integer-mm coordinates make duplicate
+    nearest points and distance ties common."""
+    import torch
+    from navslam.synth import l9_pair
+    src, tgt = l9_pair(24, 640, seed=21, integer_mm=integer_mm)
+    R, Cc = src.shape[:2]
+    dev = torch.device("cuda", 0)
+    ss, ts = torch.from_numpy(src).to(dev), torch.from_numpy(tgt).to(dev)
+    tree = torch.empty_like(ts)
+    tcol = torch.empty((R, Cc), dtype=torch.int32, device=dev)
+    tn = torch.empty(R, dtype=torch.int32, device=dev)
+    pos = torch.empty((R, Cc), dtype=torch.int32, device=dev)
+    dist = torch.empty((R, Cc), dtype=torch.float64, device=dev)
+    keep = torch.empty((R, Cc), dtype=torch.int32, device=dev)
+    sums = torch.empty((R, 6), dtype=torch.float64, device=dev)
+    torch.cuda.synchronize()
+    gpu.kd_build_rows_dev(ts, ts, R, Cc, tree, tcol, tn)
+    gpu.kd_query_rows_dev(tree, tn, ss, ss, R, Cc, pos, dist)
+    gpu.rows_corr_dev(tree, tn, pos, dist, ss, R, Cc, keep, sums)
+    gpu.sync()
+    ek, es = _dedup_reference(tree.cpu().numpy(), tn.cpu().numpy(), pos.cpu().numpy(),
+                              dist.cpu().numpy(), src)
+    _eq(keep.cpu().numpy(), ek, "kept correspondences")
+    np.testing.assert_allclose(sums.cpu().numpy(), es, rtol=1e-12, atol=1e-9)
+    assert ek.sum() > 0 and (ek.sum() < (pos.cpu().numpy() >= 0).sum() or not integer_mm)
+
+
+@pytest.mark.parametrize("R,Cc,F,steps", [(54, 42, 4, 9), (128, 2048, 3, 4)])
+def test_shim_l9_stream_fast_adam(monkeypatch, R, Cc, F, steps):
+    """NAVSLAM_ADAM=fast (GPU dedup + closed-form Adam sums) on the K5 loop:
+    the same correspondence counts as the oracle's slam.c restatement every
+    frame, poses within 1e-6 mm / deg (tolerance of the order-free sums,
+    which round differently from the reference's sequential ones)."""
+    monkeypatch.setenv("NAVSLAM_QUIET", "1")
+    monkeypatch.setenv("NAVSLAM_ADAM", "fast")
+    from pyoracle import Oracle, OracleSlam
+    from shimlib import Pos, Shim
+    from navslam.synth import l9_stream, l9_stream_index
+    frames = l9_stream(R, Cc, F, seed=17)
+    sh = Shim(R, Cc)
+    attr = sh.SLAMAttr()
+    pcs = [sh.cloud(f) for f in frames]
+    zero = np.zeros(6)
+    sh.L.init_slam(C.byref(attr), Pos.of(zero), C.byref(pcs[0]))
+    s = OracleSlam(Oracle(), R, Cc)
+    s.init(zero, frames[0])
+    last_g, last_o = Pos.of(zero), zero
+    for i in range(1, steps + 1):
+        f = l9_stream_index(i, F)
+        meas = sh.L.slam_localization(C.byref(attr), C.byref(pcs[f]), last_g, last_g)
+        sh.L.slam_mapping(C.byref(attr), meas, C.byref(pcs[f]))
+        om, iters, ncp = s.localization(frames[f], last_o, last_o)
+        s.mapping(om, frames[f])
+        np.testing.assert_allclose(np.array(meas.tolist()), om, rtol=0, atol=1e-6,
+                                   err_msg=f"frame {i} pose")
+        q, cp, it = sh.last_frame_stats()
+        assert cp == ncp, f"frame {i}: {cp} correspondences vs {ncp}"
+        assert abs(attr.error - s.error) <= 1e-9 * max(1.0, s.error)
+        last_g, last_o = meas, om
+
+
 def test_shim_kdtree_api_matches_reference_golden(golden):
     from shimlib import KDNode, Point, Shim, preorder
     sh = Shim(8, 8)
