@@ -756,18 +756,29 @@ __global__ __launch_bounds__(kRowsBlock) void k_rows_build(
   if (threadIdx.x == 0) tree_n[r] = n;
 }
 
-__global__ __launch_bounds__(kRowsBlock) void k_rows_query(
+// Per-row 1-NN, each row's columns split over gridDim.y workgroups so a
+// frame of R rows fills the chip (R = 128 rows alone would occupy half the
+// CUs): every split loads the row's whole tree into LDS (SoA) and its own
+// column slice of the query row plus the 2-column curvature halo.
+constexpr int kRowsQBlock = 256;
+
+__host__ __device__ inline int rows_query_lds(int C, int w) {
+  return align16(24 * C) + align16(24 * (w + 4)) + 4 * kRowsQBlock * kStackDepth;
+}
+
+__global__ __launch_bounds__(kRowsQBlock) void k_rows_query(
     const double *__restrict__ tree_pts, const int32_t *__restrict__ tree_n,
     const double *__restrict__ feat_src, const double *__restrict__ queries,
     int R, int C, int32_t *__restrict__ nn_pos, double *__restrict__ nn_dist,
     int32_t *__restrict__ mask_out) {
-  const RowsLds L = rows_lds(C, kRowsBlock, true);
   const int r = blockIdx.x;
+  const int w = (C + (int)gridDim.y - 1) / (int)gridDim.y;
+  const int c0 = (int)blockIdx.y * w, c1 = min(C, c0 + w);
+  if (c0 >= c1) return;
   const size_t rowoff = (size_t)r * C;
-  double *raw = (double *)(smem + L.raw);
-  double *TX = (double *)(smem + L.fc), *TY = TX + C, *TZ = TX + 2 * C;
-  uint16_t *QM = (uint16_t *)(smem + L.p);
-  uint32_t *stk = (uint32_t *)(smem + L.stk);
+  double *TX = (double *)smem, *TY = TX + C, *TZ = TX + 2 * C;
+  double *rs = (double *)(smem + align16(24 * C));
+  uint32_t *stk = (uint32_t *)(smem + align16(24 * C) + align16(24 * (w + 4)));
   const int n = tree_n[r];
   for (int pos = threadIdx.x; pos < n; pos += blockDim.x) {
     const double *t = tree_pts + 3 * (rowoff + pos);
@@ -775,18 +786,19 @@ __global__ __launch_bounds__(kRowsBlock) void k_rows_query(
     TY[pos] = t[1];
     TZ[pos] = t[2];
   }
-  block_copy(raw, feat_src + 3 * rowoff, 3 * C);
+  const int lo = max(c0 - 2, 0), hi = min(c1 + 2, C);  // slice + curvature halo
+  block_copy(rs, feat_src + 3 * (rowoff + lo), 3 * (hi - lo));
   __syncthreads();
-  for (int j = threadIdx.x; j < C; j += blockDim.x) {
-    const int f = row_curv_lds(raw, C, j) > 0.1 ? 1 : 0;
-    QM[j] = (uint16_t)f;
+  for (int j = c0 + (int)threadIdx.x; j < c1; j += blockDim.x) {
+    int f = 0;
+    if (j >= 2 && j < C - 2) {  // src/slam.c:16 window
+      const double *cj = rs + 3 * (j - lo);
+      f = curvature5(cj, cj - 6, cj - 3, cj + 3, cj + 6) > 0.1 ? 1 : 0;
+    }
     if (mask_out) mask_out[rowoff + j] = f;
-  }
-  __syncthreads();
-  for (int j = threadIdx.x; j < C; j += blockDim.x) {
     int bpos = -1;
     double bd = INFINITY;
-    if (QM[j]) {
+    if (f) {
       const double *q = queries + 3 * (rowoff + j);
       kd_query(TX, TY, TZ, n, q[0], q[1], q[2], stk + threadIdx.x, blockDim.x,
                &bpos, &bd);
@@ -2591,12 +2603,20 @@ int navgpu_kd_query_rows_dev(navgpu_ctx *ctx, const double *tree_pts,
   RC(check_rows_shape(R, C, true));
   if ((size_t)R * C == 0) return NAVGPU_OK;
   ARG_CHECK(tree_pts && tree_n && feat_src && queries && nn_pos && nn_dist);
-  const RowsLds L = rows_lds(C, kRowsBlock, true);
-  RC(set_lds(k_rows_query, L.total));
+  // column splits per row: >= 512 workgroups in all (2 per CU), slices of at
+  // least 256 columns (one per thread)
+  int S = 1;
+  while (S < 8 && (long long)R * S < 512 && C / (2 * S) >= kRowsQBlock) S <<= 1;
+  const int w = (C + S - 1) / S;
+  const int lds = rows_query_lds(C, w);
+  if (lds > lds_limit()) {
+    set_err("rows_query: C=%d needs %d B of LDS (device limit %d)", C, lds, lds_limit());
+    return NAVGPU_ERANGE;
+  }
+  RC(set_lds(k_rows_query, lds));
   TimedRegion tr(ctx, "rows_query");
-  hipLaunchKernelGGL(k_rows_query, dim3(R), dim3(kRowsBlock), L.total,
-                     ctx->stream, tree_pts, tree_n, feat_src, queries, R, C,
-                     nn_pos, nn_dist, mask_out);
+  hipLaunchKernelGGL(k_rows_query, dim3(R, S), dim3(kRowsQBlock), lds, ctx->stream,
+                     tree_pts, tree_n, feat_src, queries, R, C, nn_pos, nn_dist, mask_out);
   CHECK_LAUNCH("k_rows_query");
   return NAVGPU_OK;
 }
