@@ -57,9 +57,12 @@ __device__ unsigned long long g_stamps[16];
 #define NV_STAMP(v) const unsigned long long v = __builtin_amdgcn_s_memtime()
 #define NV_STAMP_ADD(slot, a, b) \
   if ((threadIdx.x & 63) == 0) atomicAdd(&g_stamps[slot], (b) - (a))
+#define NV_STAMP_ADD0(slot, a, b) \
+  if (threadIdx.x == 0) atomicAdd(&g_stamps[slot], (b) - (a))
 #else
 #define NV_STAMP(v)
 #define NV_STAMP_ADD(slot, a, b)
+#define NV_STAMP_ADD0(slot, a, b)
 #endif
 
 // ------------------------------------------------------------------ errors
@@ -428,11 +431,14 @@ __device__ void block_build_kdtree(const double *FC, size_t NS, int n,
   for (int i = threadIdx.x; i < n; i += blockDim.x) P[i] = (IdxT)i;
   __syncthreads();
   int depth = 0;
+  NV_STAMP(kb0);
   if (!GMEM && n >= kBlockNthMin && blockDim.x <= kBlockNthMax) {
     // the root partition by the whole block
     block_nth_element<IdxT>(FC + (depth0 % 3) * NS, P, T, 0, n - 1, n / 2);
     depth = 1;
   }
+  NV_STAMP(kb1);
+  NV_STAMP_ADD0(9, kb0, kb1);
   for (; (n >> depth) >= 2; ++depth) {
     if ((n >> depth) < kLaneSubtree) break;  // every range at this depth is <= n >> depth
     const double *key = FC + ((depth0 + depth) % 3) * NS;
@@ -445,6 +451,8 @@ __device__ void block_build_kdtree(const double *FC, size_t NS, int n,
     }
     __syncthreads();
   }
+  NV_STAMP(kb2);
+  NV_STAMP_ADD0(10, kb1, kb2);
   if (n >= 2) {
     const int roots = 1 << depth;
     for (int k = threadIdx.x; k < roots; k += blockDim.x) {
@@ -464,6 +472,9 @@ __device__ void block_build_kdtree(const double *FC, size_t NS, int n,
     if (GMEM) __threadfence_block();
     __syncthreads();
   }
+  NV_STAMP(kb3);
+  NV_STAMP_ADD0(11, kb2, kb3);
+  NV_STAMP_ADD0(12, 0ull, 1ull);
 }
 
 // Stack entry of the far subtree still to visit: [flo, fhi) at depth d; the
@@ -566,6 +577,7 @@ __device__ int row_stage_and_build(const double *feat_src, const double *coords,
   uint16_t *MK = (uint16_t *)(smem + L.t);
   int *scan = (int *)(smem + L.scan);
   const size_t rowoff = (size_t)r * C;
+  NV_STAMP(rs0);
   block_copy(raw, feat_src + 3 * rowoff, 3 * C);
   __syncthreads();
   for (int j = threadIdx.x; j < C; j += blockDim.x) {
@@ -585,6 +597,8 @@ __device__ int row_stage_and_build(const double *feat_src, const double *coords,
         FC[2 * NS + pos] = s[2];
         FCOL[pos] = (uint16_t)j;
       });
+  NV_STAMP(rs1);
+  NV_STAMP_ADD0(8, rs0, rs1);
 #ifdef NAVGPU_DBG_ROWS_NOBUILD  // timing-only ablation: identity "tree"
   for (int i = threadIdx.x; i < n; i += blockDim.x) P[i] = (uint16_t)i;
   __syncthreads();
@@ -728,6 +742,117 @@ __global__ __launch_bounds__(kRowsBlock) void k_rows_match(
     kd_query(TX, TY, TZ, n, sraw[3 * c], sraw[3 * c + 1], sraw[3 * c + 2],
              stk + threadIdx.x, blockDim.x, &bpos, &bd);
 #endif
+    nn_idx[rowoff + c] = bpos >= 0 ? pair_row0 + (int)T[bpos] : -1;
+    nn_dist[rowoff + c] = bd;
+  }
+}
+
+// K4 batches: the same fused row step with a lean LDS footprint, so that
+// several rows share a CU. A row's step is a latency chain (the reference's
+// Lomuto passes, then dependent tree walks), so a batch's throughput is set
+// by how many rows run on a CU at once. The resident k_rows_match (512
+// threads, ~136 KB) fits one per CU. This variant fits two: NT = 256
+// threads, the curvature reads the rows straight from global memory (L2)
+// instead of staging them, and the tree is permuted in place. Its LDS is the
+// SoA features (24 C), FCOL/P/T (6 C) and the walk stacks (4 NT x 14).
+// Results are identical to k_rows_match.
+constexpr int kLeanMaxC = 2048;  // in-place permutation: <= kLeanMaxC / NT per thread
+
+__host__ __device__ inline int rows_lean_lds(int C, int nt) {
+  return align16(24 * C) + 3 * align16(2 * C) + align16(4 * nt * kStackDepth) + align16(4 * 40);
+}
+
+// src/slam.c:16-58 for column j of a row read from global memory
+__device__ __forceinline__ int row_feature_global(const double *row, int C, int j) {
+  if (j < 2 || j >= C - 2) return 0;
+  const double *c = row + 3 * j;
+  return curvature5(c, c - 6, c - 3, c + 3, c + 6) > 0.1 ? 1 : 0;
+}
+
+template <int NT>
+__global__ __launch_bounds__(NT) void k_rows_match_lean(
+    const double *__restrict__ src, const double *__restrict__ tgt, int R,
+    int C, int32_t *__restrict__ src_mask, int32_t *__restrict__ tgt_mask,
+    int32_t *__restrict__ nn_idx, double *__restrict__ nn_dist) {
+  constexpr int kHold = kLeanMaxC / NT;
+  const int r = blockIdx.x;
+  const size_t rowoff = (size_t)r * C;
+  const int pair_row0 = (r % R) * C;
+  double *FC = (double *)smem;
+  uint16_t *FCOL = (uint16_t *)(smem + align16(24 * C));
+  uint16_t *P = (uint16_t *)(smem + align16(24 * C) + align16(2 * C));
+  uint16_t *T = (uint16_t *)(smem + align16(24 * C) + 2 * align16(2 * C));
+  uint32_t *stk = (uint32_t *)(smem + align16(24 * C) + 3 * align16(2 * C));
+  int *scan = (int *)(smem + align16(24 * C) + 3 * align16(2 * C) +
+                      align16(4 * NT * kStackDepth));
+  // target row: features (flag in T), compacted SoA in column order
+  const double *tg = tgt + 3 * rowoff;
+  for (int j = threadIdx.x; j < C; j += NT) {
+    const int f = row_feature_global(tg, C, j);
+    T[j] = (uint16_t)f;
+    if (tgt_mask) tgt_mask[rowoff + j] = f;
+  }
+  __syncthreads();
+  const int n = block_compact(
+      C, scan, [&](int j) { return T[j] != 0; },
+      [&](int j, int pos) {
+        FC[pos] = tg[3 * j];
+        FC[C + pos] = tg[3 * j + 1];
+        FC[2 * C + pos] = tg[3 * j + 2];
+        FCOL[pos] = (uint16_t)j;
+      });
+  block_build_kdtree<uint16_t>(FC, C, n, P, T, 0);
+  // the tree in position order, in place: every old value is read into
+  // registers before the barrier, then written to its position
+  {
+    double hx[kHold], hy[kHold], hz[kHold];
+    uint16_t hc[kHold];
+#pragma unroll
+    for (int u = 0; u < kHold; ++u) {
+      const int pos = (int)threadIdx.x + u * NT;
+      if (pos < n) {
+        const int e = P[pos];
+        hx[u] = FC[e];
+        hy[u] = FC[C + e];
+        hz[u] = FC[2 * C + e];
+        hc[u] = FCOL[e];
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < kHold; ++u) {
+      const int pos = (int)threadIdx.x + u * NT;
+      if (pos < n) {
+        FC[pos] = hx[u];
+        FC[C + pos] = hy[u];
+        FC[2 * C + pos] = hz[u];
+        T[pos] = hc[u];
+      }
+    }
+  }
+  // source row: feature flags in P, query list in FCOL
+  const double *sg = src + 3 * rowoff;
+  for (int j = threadIdx.x; j < C; j += NT) {
+    const int f = row_feature_global(sg, C, j);
+    P[j] = (uint16_t)f;
+    if (src_mask) src_mask[rowoff + j] = f;
+    if (!f) {
+      nn_idx[rowoff + j] = -1;
+      nn_dist[rowoff + j] = INFINITY;
+    }
+  }
+  __syncthreads();
+  uint16_t *QL = FCOL;
+  const int nq = block_compact(
+      C, scan, [&](int j) { return P[j] != 0; },
+      [&](int j, int pos) { QL[pos] = (uint16_t)j; });
+  const double *TX = FC, *TY = FC + C, *TZ = FC + 2 * C;
+  for (int i = threadIdx.x; i < nq; i += NT) {
+    const int c = QL[i];
+    int bpos;
+    double bd;
+    kd_query(TX, TY, TZ, n, sg[3 * c], sg[3 * c + 1], sg[3 * c + 2], stk + threadIdx.x, NT,
+             &bpos, &bd);
     nn_idx[rowoff + c] = bpos >= 0 ? pair_row0 + (int)T[bpos] : -1;
     nn_dist[rowoff + c] = bd;
   }
@@ -2669,9 +2794,20 @@ int navgpu_rows_match_batch_dev(navgpu_ctx *ctx, const double *src,
   ARG_CHECK((long long)npairs * R <= INT32_MAX && (long long)npairs * R * C < INT32_MAX);
   if ((size_t)npairs * R * C == 0) return NAVGPU_OK;
   ARG_CHECK(src && tgt && nn_idx && nn_dist);
+  TimedRegion tr(ctx, "rows_match");
+  // enough rows to fill the chip several times over: the lean variant (two
+  // rows per CU); a short batch keeps the 512-thread kernel (lower latency
+  // per row)
+  if (C <= kLeanMaxC && (long long)npairs * R >= 1024 && !getenv("NAVGPU_ROWS_NO_LEAN")) {
+    const int lds = rows_lean_lds(C, 256);
+    RC(set_lds(k_rows_match_lean<256>, lds));
+    hipLaunchKernelGGL(k_rows_match_lean<256>, dim3(npairs * R), dim3(256), lds, ctx->stream,
+                       src, tgt, R, C, src_mask, tgt_mask, nn_idx, nn_dist);
+    CHECK_LAUNCH("k_rows_match_lean");
+    return NAVGPU_OK;
+  }
   const RowsLds L = rows_lds(C, kRowsBlock, true);
   RC(set_lds(k_rows_match, L.total));
-  TimedRegion tr(ctx, "rows_match");
   hipLaunchKernelGGL(k_rows_match, dim3(npairs * R), dim3(kRowsBlock), L.total,
                      ctx->stream, src, tgt, R, C, src_mask, tgt_mask, nn_idx,
                      nn_dist);

@@ -51,4 +51,15 @@ out = {
     "queries_mean": float(sm.float().sum(1).mean().item()),
 }
 out["lib"] = os.path.basename(sys.argv[1]) if len(sys.argv) > 1 else "libnavgpu.so"
+import ctypes  # noqa: E402
+st = (ctypes.c_ulonglong * 16)()
+if g.L.navgpu_debug_stamps(st) == 0:  # NAVGPU_STAMPS builds: one clean build call
+    g.kd_build_rows_dev(tgt, tgt, R, C, tp, tc, tn, tm)
+    torch.cuda.synchronize()
+    g.L.navgpu_debug_stamps(st)
+    nb = max(int(st[12]), 1)
+    out["stamps_cycles_per_row"] = {"stage+curv+compact": int(st[8]) // nb,
+                                    "root(block)": int(st[9]) // nb,
+                                    "wave levels": int(st[10]) // nb,
+                                    "lane tail": int(st[11]) // nb, "rows": nb}
 print(json.dumps(out))

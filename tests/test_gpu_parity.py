@@ -144,6 +144,37 @@ def test_rows_match_batch_equals_per_pair(gpu, orc):
             _eq(x, y, f"pair {p} {name}")
 
 
+def test_rows_match_batch_lean_path(gpu, orc, monkeypatch):
+    """A batch of >= 1024 rows takes the lean two-rows-per-CU kernel
+    (k_rows_match_lean): same masks, indices and distances as the oracle and
+    as the resident kernel (NAVGPU_ROWS_NO_LEAN=1)."""
+    import torch
+    from navslam.synth import l9_pair
+    R, Cc, P = 64, 300, 16
+    pairs = [l9_pair(R, Cc, seed=60 + p, integer_mm=p % 3 == 1) for p in range(P)]
+    dev = torch.device("cuda", 0)
+    src = torch.from_numpy(np.stack([a for a, _ in pairs])).to(dev)
+    tgt = torch.from_numpy(np.stack([b for _, b in pairs])).to(dev)
+
+    def run():
+        i32 = lambda: torch.full((P, R, Cc), -7, dtype=torch.int32, device=dev)  # noqa: E731
+        sm, tm, idx = i32(), i32(), i32()
+        dist = torch.zeros((P, R, Cc), dtype=torch.float64, device=dev)
+        gpu.rows_match_batch_dev(src, tgt, P, R, Cc, sm, tm, idx, dist)
+        torch.cuda.synchronize()
+        return [t.cpu().numpy() for t in (sm, tm, idx, dist)]
+    lean = run()
+    monkeypatch.setenv("NAVGPU_ROWS_NO_LEAN", "1")
+    resident = run()
+    names = ("src_mask", "tgt_mask", "nn_idx", "nn_dist")
+    for x, y, name in zip(lean, resident, names):
+        _eq(x, y, f"lean vs resident {name}")
+    for p in (0, 1, P - 1):
+        ref = orc.rows_match(*pairs[p])
+        for x, y, name in zip(lean, ref, names):
+            _eq(x[p], y, f"pair {p} {name}")
+
+
 def test_rows_match_edge_cases(gpu, orc):
     rng = np.random.default_rng(5)
     cases = [np.zeros((3, 5, 3)),                                   # C < 5: no window
