@@ -1589,6 +1589,7 @@ struct KnnLists {
   int *ovf_tiles, *n_ovf;  // tiles whose segments overflow the LDS budget
   int *slow_q, *n_slow;    // queries the fast path could not certify
   double *slow_thr;        // their starting bound (K-th dsq upper bound)
+  int vec_out;             // outputs 16-B aligned: k_knn may store them as vectors
 };
 
 typedef float f2 __attribute__((ext_vector_type(2)));
@@ -1768,7 +1769,8 @@ __device__ __forceinline__ void knn_one(
       const double dsq = (double)__uint_as_float(key[s] & ~kKeyMask) + gpos[s] * 1e-30;
 #else
       const double *tp = tsort + 3 * (size_t)gpos[s];
-      const double ddx = tp[0] - qv[0], ddy = tp[1] - qv[1], ddz = tp[2] - qv[2];
+      const double px = tp[0], py = tp[1], pz = tp[2];
+      const double ddx = px - qv[0], ddy = py - qv[1], ddz = pz - qv[2];
       const double dsq = ddx * ddx + ddy * ddy + ddz * ddz;  // utils/kdtree.c:16
 #endif
       ed[s] = ei[s] >= 0 ? __builtin_sqrt(dsq) : INFINITY;
@@ -1786,13 +1788,23 @@ __device__ __forceinline__ void knn_one(
       ei[s] = -1;
     }
   }
-  // order by (distance, index): the f32 order is almost always already right
+  // order by (distance, index): the truncated-key order is almost always
+  // right, and a misordered survivor sits next to its place. Bubble passes
+  // run until no lane of the wave is out of order, usually one: some lane of
+  // a wave is misordered about every other batch, so a fixed KL-1 passes
+  // cost a large share of the scan (NAVGPU_SORT_FIXED restores them).
   bool sorted = true;
 #pragma unroll
   for (int s = 1; s < KL; ++s) sorted &= !knn_less(ed[s], ei[s], ed[s - 1], ei[s - 1]);
-  if (!sorted) {  // rare: bubble passes (a fixed-trip loop keeps VGPRs low)
+#ifdef NAVGPU_SORT_FIXED
+  if (!sorted) {
 #pragma unroll 1
     for (int pass = 0; pass < KL - 1; ++pass) {
+#else
+  {
+#pragma unroll 1
+    for (int pass = 0; pass < KL - 1 && __any(!sorted); ++pass) {
+#endif
 #pragma unroll
       for (int u = 1; u < KL; ++u) {
         const bool sw = knn_less(ed[u], ei[u], ed[u - 1], ei[u - 1]);
@@ -1803,6 +1815,11 @@ __device__ __forceinline__ void knn_one(
         ed[u - 1] = sw ? td : ed[u - 1];
         ei[u - 1] = sw ? ti : ei[u - 1];
       }
+#ifndef NAVGPU_SORT_FIXED
+      sorted = true;
+#pragma unroll
+      for (int s = 1; s < KL; ++s) sorted &= !knn_less(ed[s], ei[s], ed[s - 1], ei[s - 1]);
+#endif
     }
   }
   const double dk = ed[K - 1];
@@ -1826,6 +1843,19 @@ __device__ __forceinline__ void knn_one(
     }
     oidx[q * K] = iacc + (int)acc;
 #else
+    // a query's K results are contiguous: 16-B stores when K allows and the
+    // host found both outputs 16-B aligned (L_.vec_out)
+    if constexpr (K % 4 == 0) {
+      if (L_.vec_out) {
+#pragma unroll
+        for (int s = 0; s < K; s += 4)
+          *(int4 *)(oidx + q * K + s) = make_int4(ei[s], ei[s + 1], ei[s + 2], ei[s + 3]);
+#pragma unroll
+        for (int s = 0; s < K; s += 2)
+          *(double2 *)(odist + q * K + s) = make_double2(ed[s], ed[s + 1]);
+        return;
+      }
+    }
 #pragma unroll
     for (int s = 0; s < K; ++s) {
       oidx[q * K + s] = ei[s];
@@ -3032,6 +3062,10 @@ static int knn_run(navgpu_ctx *ctx, const double *tgt, size_t nt, const double *
   RC(ws(ctx, kSlowThr, nq, &lists.slow_thr));
   lists.n_ovf = counters;
   lists.n_slow = counters + 1;
+  lists.vec_out = ((uintptr_t)idx % 16 == 0 && (uintptr_t)dist % 16 == 0) ? 1 : 0;
+#ifdef NAVGPU_SCALAR_OUT
+  lists.vec_out = 0;
+#endif
   TimedRegion tr(ctx, "knn_query");
   // tiles are walked by a grid of 8 x nbx blocks (block b -> XCD b % 8, the
   // placement HW_REG_XCC_ID reports); more blocks than resident slots

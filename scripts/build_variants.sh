@@ -9,9 +9,10 @@ build() {  # build <name> <defines...>
     -Iinclude "$@" -shared -o "nav-slam_amd/lib/variants/libnavgpu_$name.so" \
     nav-slam_amd/csrc/navgpu.hip &
 }
-build base
-build noblock -DNAVGPU_BLOCK_NTH_MIN=1000000
-build rows_noquery -DNAVGPU_DBG_ROWS_NOQUERY
-build noblock_noquery -DNAVGPU_BLOCK_NTH_MIN=1000000 -DNAVGPU_DBG_ROWS_NOQUERY
+build new
+build old -DNAVGPU_SORT_FIXED -DNAVGPU_SCALAR_OUT
+build sortfixed -DNAVGPU_SORT_FIXED
+build scalarout -DNAVGPU_SCALAR_OUT
+
 wait
 ls nav-slam_amd/lib/variants
