@@ -31,6 +31,7 @@ F=$(find "$OUT/pmc_fetch" -name "*counter_collection.csv" | head -1)
 W=$(find "$OUT/pmc_write" -name "*counter_collection.csv" | head -1)
 step traffic 120 python3 scripts/traffic_json.py "$F" "$W" "$OUT/traffic_k3.json" "$TAG"
 step bench 600 python3 bench.py --traffic-json "$OUT/traffic_k3.json" --json-out "$OUT/bench.json"
+step bench_inflight1 300 python3 bench.py --inflight 1 --no-cpu-baseline --traffic-json "$OUT/traffic_k3.json" --json-out "$OUT/bench_inflight1.json"
 step bench_k2 300 python3 bench.py --workload k2 --steps 10 --json-out "$OUT/bench_k2.json"
 step bench_k4 300 python3 bench.py --workload k4 --steps 3 --warmup 1 --json-out "$OUT/bench_k4.json"
 step trace_k4 300 rocprofv3 --kernel-trace --stats -d "$OUT/trace_k4" -o run --output-format csv -- python3 bench.py --workload k4 --steps 3 --warmup 1 --no-cpu-baseline
