@@ -19,7 +19,11 @@ Checks:
   * GPU: at 8x8 the shim-linked program's stdout and CSV byte-identical to
     the reference program's; at 64x512 (the BASELINE K1 grid, where the
     reference cannot be built: utils/pointcloud.h:9-10 fixes 8x8) its CSV
-    identical to the oracle replay.
+    identical to the oracle replay;
+  * the same for main.c's L9 handler (CSV frames in, the L9 loop, CSV out),
+    which main() never calls: nav_slam_l9_* link oracle/k1_l9_main.c, a
+    main() that calls it, at 8x8 (against the reference program) and at the
+    L9 grid 54x42 (against the replay).
 """
 import ctypes as C
 import json
@@ -235,3 +239,104 @@ def test_k1_main_on_shim_64x512_matches_oracle(tmp_path):
     depth, imu, ts = stream(R, Cc, F, seed=3)
     _, csv = run_main(exe("nav_slam_gpu_64x512"), str(tmp_path), depth, imu, ts)
     check_csv(csv, replay_rows(depth, imu, ts), R, Cc, F)
+
+
+# ---------------------------------------------- the L9 handler of main.c
+# src/main.c:362-472: the L9 CSV reader (frame,row,col,x,y,z,conf in integer
+# mm, the visualization/parse_dataset.py format), the L9 SLAM loop
+# (localization with pred = last, then mapping at the measured pose,
+# src/main.c:423-431) and its CSV writer. main() never calls it
+# (src/main.c:477-481), so oracle/k1_l9_main.c is a main() that does. The
+# writer passes int 0 to %.2f (src/main.c:399-417): those columns are
+# undefined behaviour and are compared only between two builds of the same
+# main.c, never against the replay.
+def l9_frames(R, Cc, F, seed):
+    """Integer-mm frames [F, R, C, 3] in which every row of every frame has a
+    feature: with an empty row tree the reference reads an uninitialised
+    Point (src/slam.c:242-252), undefined behaviour no build can match. 8x8:
+    the L5 test scene projected (utils/pointcloud.c:8-48); larger grids: the
+    ray-cast L9 walk."""
+    from pyoracle import Oracle
+    from navslam.synth import l5_stream, l9_stream
+    orc = Oracle()
+    for s in range(seed, seed + 50):
+        if R == 8:
+            depth, _ = l5_stream(np.random.default_rng(s), F, R=R, C=Cc)
+            fr = np.stack([orc.convert(d) for d in depth])
+        else:
+            fr = l9_stream(R, Cc, F, seed=s, step=(60.0, 20.0, 0.0), yaw_step_deg=0.5)
+        fr = np.rint(fr).astype(np.int64)  # what fscanf("%lf") reads back: no -0.0
+        if all(orc.extract_feature(f.astype(np.float64)).any(axis=1).all() for f in fr):
+            return fr
+    raise AssertionError("no stream with a feature in every row")
+
+
+def run_l9(binary, workdir, fr):
+    os.makedirs(workdir, exist_ok=True)
+    F, R, Cc, _ = fr.shape
+    lines = ["frame,row,col,x,y,z,conf"]
+    for f in range(F):
+        for r in range(R):
+            for c in range(Cc):
+                x, y, z = fr[f, r, c]
+                lines.append(f"{f},{r},{c},{x},{y},{z},{(r * 7 + c) % 100}")
+    with open(os.path.join(workdir, "parsed_data.csv"), "w") as fh:
+        fh.write("\n".join(lines) + "\n")
+    p = subprocess.run([binary], cwd=workdir, capture_output=True, preexec_fn=_big_stack,
+                       timeout=300, env={k: v for k, v in os.environ.items()
+                                         if k != "NAVSLAM_QUIET"})
+    assert p.returncode == 0, p.stderr.decode(errors="replace")[-2000:]
+    with open(os.path.join(workdir, "point_cloud_data.csv")) as fh:
+        return p.stdout, fh.read().splitlines()
+
+
+def replay_l9_xyz(fr):
+    """src/main.c:380-431 over the oracle: per frame the global cloud, as the
+    CSV's first six columns (ts, row, col, x, y, z)."""
+    from pyoracle import Oracle, OracleSlam
+    orc = Oracle()
+    F, R, Cc, _ = fr.shape
+    fd = fr.astype(np.float64)
+    s = OracleSlam(orc, R, Cc)
+    z = np.zeros(6)
+    s.init(z, fd[0])
+    globs = [s.last_global()]
+    last = z
+    for i in range(1, F):
+        meas, _, _ = s.localization(fd[i], last, last)
+        s.mapping(meas, fd[i])
+        globs.append(s.last_global())
+        last = meas
+    return ["%d,%d,%d,%.2f,%.2f,%.2f" % (f, r, c, *globs[f][r, c])
+            for f in range(F) for r in range(R) for c in range(Cc)]
+
+
+def check_l9_xyz(csv, fr):
+    F, R, Cc, _ = fr.shape
+    assert len(csv) == 1 + F * R * Cc
+    got = [",".join(line.split(",")[:6]) for line in csv[1:]]
+    want = replay_l9_xyz(fr)
+    bad = [i for i, (a, b) in enumerate(zip(got, want)) if a != b]
+    assert not bad, f"{len(bad)} rows differ, first: {got[bad[0]]!r} vs {want[bad[0]]!r}"
+
+
+def test_k1_l9_reference_main_matches_oracle_replay(tmp_path):
+    fr = l9_frames(8, 8, 6, seed=4)
+    _, csv = run_l9(exe("nav_slam_l9_ref_8x8"), str(tmp_path), fr)
+    check_l9_xyz(csv, fr)
+
+
+@pytest.mark.gpu
+def test_k1_l9_main_on_shim_matches_reference_main_8x8(tmp_path):
+    fr = l9_frames(8, 8, 8, seed=6)
+    out_ref, csv_ref = run_l9(exe("nav_slam_l9_ref_8x8"), str(tmp_path / "ref"), fr)
+    out_gpu, csv_gpu = run_l9(exe("nav_slam_l9_gpu_8x8"), str(tmp_path / "gpu"), fr)
+    assert csv_gpu == csv_ref
+    assert out_gpu == out_ref
+
+
+@pytest.mark.gpu
+def test_k1_l9_main_on_shim_54x42_matches_oracle(tmp_path):
+    fr = l9_frames(54, 42, 10, seed=8)  # lidarData[10] holds 10 frames (src/main.c:363)
+    _, csv = run_l9(exe("nav_slam_l9_gpu_54x42"), str(tmp_path), fr)
+    check_l9_xyz(csv, fr)
