@@ -1754,7 +1754,11 @@ __device__ __forceinline__ void knn_one(
     for (int s = 0; s < KL; ++s) {
       const bool v = key[s] != kNoKey;
       const int l = (int)((v ? key[s] : key[0]) & kKeyMask);
+#ifdef NAVGPU_DBG_NODECODE  // timing-only ablation: every slot decodes in run 0
+      const int r = 0, off = l & ((1 << kRunOffBits) - 1);
+#else
       const int r = min(l >> kRunOffBits, 8), off = l & ((1 << kRunOffBits) - 1);
+#endif
       int t0, t1, g0;
       runs(r, t0, t1, g0);
       // record, in the fetch index space; clamped into the run so that a
@@ -1796,7 +1800,11 @@ __device__ __forceinline__ void knn_one(
   bool sorted = true;
 #pragma unroll
   for (int s = 1; s < KL; ++s) sorted &= !knn_less(ed[s], ei[s], ed[s - 1], ei[s - 1]);
-#ifdef NAVGPU_SORT_FIXED
+#if defined(NAVGPU_DBG_NOSORT)  // timing-only ablation: no ordering pass
+  if (false) {
+#pragma unroll 1
+    for (int pass = 0; pass < KL - 1; ++pass) {
+#elif defined(NAVGPU_SORT_FIXED)
   if (!sorted) {
 #pragma unroll 1
     for (int pass = 0; pass < KL - 1; ++pass) {
@@ -1829,7 +1837,8 @@ __device__ __forceinline__ void knn_one(
   else
     ok = ok && B == INFINITY;  // fewer than K neighbours: only if all was seen
 #if defined(NAVGPU_DBG_NOINSERT) || defined(NAVGPU_DBG_NOEXACT) || \
-    defined(NAVGPU_DBG_NOF64) || defined(NAVGPU_DBG_NOSTAGE)
+    defined(NAVGPU_DBG_NOF64) || defined(NAVGPU_DBG_NOSTAGE) || \
+    defined(NAVGPU_DBG_NODECODE) || defined(NAVGPU_DBG_NOSORT)
   ok = true;  // timing-only ablation builds: never take the slow path
 #endif
   if (ok) {

@@ -9,10 +9,12 @@ build() {  # build <name> <defines...>
     -Iinclude "$@" -shared -o "nav-slam_amd/lib/variants/libnavgpu_$name.so" \
     nav-slam_amd/csrc/navgpu.hip &
 }
-build new
-build old -DNAVGPU_SORT_FIXED -DNAVGPU_SCALAR_OUT
-build sortfixed -DNAVGPU_SORT_FIXED
-build scalarout -DNAVGPU_SCALAR_OUT
-
+build base
+build nosort -DNAVGPU_DBG_NOSORT
+build nodecode -DNAVGPU_DBG_NODECODE
+build noout -DNAVGPU_DBG_NOOUT
+build nof64 -DNAVGPU_DBG_NOF64
+build noexact -DNAVGPU_DBG_NOEXACT
+build noins -DNAVGPU_DBG_NOINSERT
 wait
 ls nav-slam_amd/lib/variants

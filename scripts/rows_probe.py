@@ -1,5 +1,8 @@
-"""K2 per-row mode timing split: fused k_rows_match vs k_rows_build +
-k_rows_query (torch events on the library's stream)."""
+"""Per-row build phases (NAVGPU_STAMPS builds): times navgpu_kd_build_rows_dev
+on K2-shaped L9 frames and prints the s_memtime phase sums of
+row_stage_and_build / block_build_kdtree (slots 8-12), per row."""
+import argparse
+import ctypes
 import json
 import os
 import sys
@@ -7,59 +10,45 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "nav-slam_amd"))
 import torch  # noqa: E402
+
 from navslam import synth  # noqa: E402
-import navslam.gpu as ng  # noqa: E402
-from navslam.gpu import NavGpu  # noqa: E402
+import navslam.gpu as G  # noqa: E402
 
-if len(sys.argv) > 1:  # --lib path: an experimental build
-    ng.load_library(sys.argv[1])
-
-R, C = 128, 2048
+ap = argparse.ArgumentParser()
+ap.add_argument("--lib", default=None)
+ap.add_argument("--rows", type=int, default=128)
+ap.add_argument("--cols", type=int, default=2048)
+ap.add_argument("--integer", action="store_true")
+a = ap.parse_args()
+if a.lib:
+    G.load_library(a.lib)
 dev = torch.device("cuda", 0)
-st = torch.cuda.current_stream(dev)
-g = NavGpu(0, st.cuda_stream)
-s_h, t_h = synth.l9_pair(R, C, seed=5)
-src = torch.from_numpy(s_h).to(dev)
-tgt = torch.from_numpy(t_h).to(dev)
-i32 = lambda: torch.empty((R, C), dtype=torch.int32, device=dev)  # noqa: E731
-sm, tm, idx = i32(), i32(), i32()
-dst = torch.empty((R, C), dtype=torch.float64, device=dev)
-tp = torch.empty((R, C, 3), dtype=torch.float64, device=dev)
-tc, pos = i32(), i32()
-tn = torch.empty(R, dtype=torch.int32, device=dev)
-
-
-def timeit(fn, reps=20):
-    # the library runs on its own stream when handed torch's default (null)
-    # stream, so time with device-wide synchronisation
-    import time
-    for _ in range(3):
-        fn()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(reps):
-        fn()
-    torch.cuda.synchronize()
-    return 1e6 * (time.perf_counter() - t0) / reps
-
-
-out = {
-    "rows_match_us": timeit(lambda: g.rows_match_dev(src, tgt, R, C, sm, tm, idx, dst)),
-    "rows_build_us": timeit(lambda: g.kd_build_rows_dev(tgt, tgt, R, C, tp, tc, tn, tm)),
-    "rows_query_us": timeit(lambda: g.kd_query_rows_dev(tp, tn, src, src, R, C, pos, dst, sm)),
-    "tree_n_mean": float(tn.float().mean().item()),
-    "queries_mean": float(sm.float().sum(1).mean().item()),
-}
-out["lib"] = os.path.basename(sys.argv[1]) if len(sys.argv) > 1 else "libnavgpu.so"
-import ctypes  # noqa: E402
+g = G.NavGpu(0, torch.cuda.current_stream(dev).cuda_stream)
+R, Cc = a.rows, a.cols
+s, t = synth.l9_pair(R, Cc, seed=5, integer_mm=a.integer)
+tgt = torch.from_numpy(t).to(dev)
+tp = torch.empty((R, Cc, 3), dtype=torch.float64, device=dev)
+tc = torch.empty((R, Cc), dtype=torch.int32, device=dev)
+tn = torch.empty((R,), dtype=torch.int32, device=dev)
+for _ in range(2):
+    g.kd_build_rows_dev(tgt, tgt, R, Cc, tp, tc, tn)
+torch.cuda.synchronize()
 st = (ctypes.c_ulonglong * 16)()
-if g.L.navgpu_debug_stamps(st) == 0:  # NAVGPU_STAMPS builds: one clean build call
-    g.kd_build_rows_dev(tgt, tgt, R, C, tp, tc, tn, tm)
-    torch.cuda.synchronize()
+have = g.L.navgpu_debug_stamps(st) == 0
+g.timing(True)
+g.kd_build_rows_dev(tgt, tgt, R, Cc, tp, tc, tn)
+torch.cuda.synchronize()
+ms, n = g.timing_read("rows_build")
+out = {"lib": os.path.basename(a.lib or "libnavgpu.so"), "build_us": 1000 * ms / max(n, 1),
+       "mean_features": float(tn.float().mean()), "max_features": int(tn.max())}
+if have:
     g.L.navgpu_debug_stamps(st)
     nb = max(int(st[12]), 1)
-    out["stamps_cycles_per_row"] = {"stage+curv+compact": int(st[8]) // nb,
-                                    "root(block)": int(st[9]) // nb,
-                                    "wave levels": int(st[10]) // nb,
-                                    "lane tail": int(st[11]) // nb, "rows": nb}
+    # s_memtime ticks per row (shader clock); shares of the row's build
+    ph = {k: int(st[i]) / nb for i, k in ((8, "stage"), (9, "root"), (10, "wave_levels"),
+                                          (11, "lane_subtrees"))}
+    tot = sum(ph.values()) or 1
+    out.update({k + "_ticks_per_row": round(v) for k, v in ph.items()})
+    out.update({k + "_share": round(v / tot, 3) for k, v in ph.items()})
+    out["rows"] = nb
 print(json.dumps(out))
