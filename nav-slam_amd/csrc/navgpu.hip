@@ -427,7 +427,7 @@ constexpr int kBlockLevelMin = NAVGPU_BLOCK_LEVEL_MIN;  // deeper levels by the 
 // long, each lane builds whole subtrees serially, level by level inside the
 // subtree (subtrees are independent, so the order of their levels is free).
 // Root axis = depth0 % 3 (kdtree.c:70, getAxis(depth)).
-template <class IdxT, bool GMEM = false>
+template <class IdxT, bool GMEM = false, bool LEVELS = true>
 __device__ void block_build_kdtree(const double *FC, size_t NS, int n,
                                    IdxT *P, IdxT *T, int depth0) {
   const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
@@ -443,10 +443,10 @@ __device__ void block_build_kdtree(const double *FC, size_t NS, int n,
     // levels whose subarrays are still long: each subarray by the whole
     // block in turn (a level of w subarrays would otherwise keep only w
     // waves busy, and its pass chain would be the longest of the build)
-    // (512+ thread blocks only: the lean 256-thread K4 kernel shares its CU
-    // with a second row, and there the waves-per-subarray form measured
-    // faster, 54.2 vs 56.7 ms per 256 pairs)
-    for (; (n >> depth) >= kBlockLevelMin && blockDim.x >= 512; ++depth) {
+    // (512+ thread blocks only; the lean 256-thread K4 kernel shares its CU
+    // with a second row and is compiled without this loop, LEVELS = false:
+    // with it, 54.2 -> 56.3 ms per 256 pairs)
+    for (; LEVELS && (n >> depth) >= kBlockLevelMin && blockDim.x >= 512; ++depth) {
       const double *key = FC + ((depth0 + depth) % 3) * NS;
       for (int k = 0; k < (1 << depth); ++k) {
         int lo, hi;
@@ -819,7 +819,7 @@ __global__ __launch_bounds__(NT) void k_rows_match_lean(
         FC[2 * C + pos] = tg[3 * j + 2];
         FCOL[pos] = (uint16_t)j;
       });
-  block_build_kdtree<uint16_t>(FC, C, n, P, T, 0);
+  block_build_kdtree<uint16_t, false, false>(FC, C, n, P, T, 0);
   // the tree in position order, in place: every old value is read into
   // registers before the barrier, then written to its position
   {
