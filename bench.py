@@ -68,7 +68,15 @@ def parse():
                         "HBM-bound index build overlaps the previous pair's issue-bound "
                         "query (measured: 1 -> 0.345 ms/pair, 2 -> 0.294, 3 -> 0.294); "
                         "--graph needs --inflight 1")
-    p.add_argument("--cpu-reps", type=int, default=3)
+    p.add_argument("--cpu-reps", type=int, default=5,
+                   help="CPU baseline: timed repetitions (median), after one untimed warm-up")
+    p.add_argument("--resident-pairs", type=int, default=9,
+                   help="k3: distinct scan pairs resident in HBM, rotated step by step "
+                        "(9 x 48 MiB = 432 MiB, above the 256 MiB Infinity Cache, so the "
+                        "inputs of a step are not the previous step's cache hits)")
+    p.add_argument("--iso-steps", type=int, default=10,
+                   help="k3: extra steps on one context alone after the timed region, "
+                        "for the isolated kernel durations")
     p.add_argument("--traffic-csv", default=None,
                    help="comma-separated rocprofv3 --pmc counter_collection.csv files "
                         "(FETCH_SIZE and WRITE_SIZE passes) to derive HBM bytes")
@@ -86,48 +94,108 @@ def dist_env():
     return ws, rank, local
 
 
-def cpu_baseline_k3(src, tgt, k, reps):
-    """The reference's own CPU path on the same pair (rank 0 only):
-    oracle/_ref/libref8x8.so = utils/kdtree.c compiled as-is (buildKDTree over
-    the 1M target, nearestNeighborSearch for every source point; the
-    reference implements k=1 only) + the oracle's bit-exact restatement of
-    extract_feature on both 512x2048 clouds (the reference's is fixed to
-    8x8). Single-threaded like the reference; median of `reps` runs."""
+def host_info():
+    """nproc, the CPU model and the threads the all-cores legs may use."""
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except AttributeError:
+        aff = os.cpu_count()
+    return {"nproc": os.cpu_count(), "affinity_cpus": aff, "cpu_model": model,
+            "omp_num_threads": os.environ.get("OMP_NUM_THREADS")}
+
+
+def median_after_warmup(fn, reps):
+    """One untimed warm-up, then the median of `reps` timed runs."""
+    fn()
+    ts = []
+    for _ in range(max(1, reps)):
+        t0 = time.perf_counter()
+        fn()
+        ts.append(time.perf_counter() - t0)
+    return float(np.median(ts)), ts
+
+
+def _ref_lib():
     import ctypes as C
+    ref_path = os.path.join(ROOT, "oracle", "_ref", "libref8x8.so")
+    if not os.path.exists(ref_path):
+        return None
+    lib = C.CDLL(ref_path)
+    lib.buildKDTree.restype = C.c_void_p
+    lib.buildKDTree.argtypes = [C.c_void_p, C.c_size_t, C.c_int]
+    lib.freeKDTree.argtypes = [C.c_void_p]
+    return lib
+
+
+def _addr(lib, name):
+    import ctypes as C
+    return C.cast(getattr(lib, name), C.c_void_p).value
+
+
+def cpu_baseline_k3(src, tgt, k, reps):
+    """The reference's own CPU path on the K3 pair (rank 0, N = 1 only):
+    oracle/_ref/libref8x8.so = utils/kdtree.c compiled as-is -- buildKDTree
+    over the 1M target (utils/kdtree.c:65-82) and nearestNeighborSearch for
+    every source point (utils/kdtree.c:110-152; the reference has k = 1 only)
+    -- plus the oracle's bit-exact restatement of extract_feature
+    (src/slam.c:11-61) on both 512x2048 clouds (the reference's own is fixed
+    to 8x8). Two legs, each the median of `reps` after one warm-up:
+      1 core    : as the reference runs (single-threaded);
+      all cores : OpenMP over the queries (the search only reads the tree)
+                  and over rows for the curvature; the tree build is the
+                  reference's serial recursion.
+    """
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     from pyoracle import Oracle
     orc = Oracle()
-    ref_path = os.path.join(ROOT, "oracle", "_ref", "libref8x8.so")
-    kind = "reference" if os.path.exists(ref_path) else "port"
+    lib = _ref_lib()
+    kind = "reference" if lib is not None else "port"
     N = src.shape[0] * src.shape[1]
-    times = []
-    for _ in range(reps):
-        t0 = time.perf_counter()
-        orc.extract_feature(src)
-        orc.extract_feature(tgt)
-        if kind == "reference":
-            lib = C.CDLL(ref_path)
-            lib.buildKDTree.restype = C.c_void_p
-            lib.buildKDTree.argtypes = [C.c_void_p, C.c_size_t, C.c_int]
-            lib.freeKDTree.argtypes = [C.c_void_p]
-            lib.nearestNeighborSearch.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p,
-                                                  C.c_void_p, C.c_int]
-            arr = np.ascontiguousarray(tgt.reshape(-1, 3)).copy()
-            root = lib.buildKDTree(arr.ctypes.data, N, 0)
-            fn = C.cast(lib.nearestNeighborSearch, C.c_void_p).value
-            orc.ref_nn_batch(fn, root, src.reshape(-1, 3))
-            lib.freeKDTree(root)
-        else:
-            t, _ = orc.kd_build(tgt.reshape(-1, 3))
-            orc.kd_nn_batch(t, src.reshape(-1, 3))
-        times.append(time.perf_counter() - t0)
-    t = float(np.median(times))
-    return {"value": N / t, "unit": "matches/s", "cores": 1, "kind": kind,
-            "seconds_per_pair": t,
-            "sample": (f"the full K3 pair ({N} queries vs {N} targets), median of {reps}: "
-                       "extract_feature on both clouds + buildKDTree + nearestNeighborSearch "
-                       "per source point, k=1 (the reference has no k-NN; k=8 would cost "
-                       "more)")}
+    q = np.ascontiguousarray(src.reshape(-1, 3))
+
+    def run(threads):
+        def once():
+            if threads == 1:
+                orc.extract_feature(src)
+                orc.extract_feature(tgt)
+            else:
+                orc.extract_feature_mt(src, threads)
+                orc.extract_feature_mt(tgt, threads)
+            if lib is not None:
+                arr = np.ascontiguousarray(tgt.reshape(-1, 3)).copy()
+                root = lib.buildKDTree(arr.ctypes.data, N, 0)
+                fn = _addr(lib, "nearestNeighborSearch")
+                (orc.ref_nn_batch if threads == 1 else orc.ref_nn_batch_mt)(fn, root, q)
+                lib.freeKDTree(root)
+            else:
+                t, _ = orc.kd_build(tgt.reshape(-1, 3))
+                orc.kd_nn_batch(t, q)
+        return once
+
+    host = host_info()
+    t1, ts1 = median_after_warmup(run(1), reps)
+    threads = orc.max_threads()
+    tall, tsall = median_after_warmup(run(threads), reps)
+    return {"value": round(N / t1, 1), "unit": "matches/s", "cores": 1, "kind": kind,
+            "seconds_per_pair": round(t1, 4), "runs_s": [round(t, 4) for t in ts1],
+            "all_cores": {"value": round(N / tall, 1), "unit": "matches/s", "cores": threads,
+                          "seconds_per_pair": round(tall, 4),
+                          "runs_s": [round(t, 4) for t in tsall],
+                          "note": "OpenMP over queries and curvature rows; serial tree build"},
+            "host": host,
+            "sample": (f"the full K3 pair 0 ({N} queries vs {N} targets), median of {reps} after "
+                       "1 warm-up: extract_feature on both clouds + buildKDTree + "
+                       "nearestNeighborSearch per source point, k=1 (the reference has no "
+                       "k-NN; k=8 would cost more)")}
 
 
 def cpu_baseline_k2(src, tgt, reps):
@@ -136,42 +204,40 @@ def cpu_baseline_k2(src, tgt, reps):
     reference's is fixed to 8x8) + for every row the reference's own
     buildKDTree over the target row's features and nearestNeighborSearch for
     each source feature (oracle/_ref = utils/kdtree.c compiled as-is), which
-    is what src/slam.c:230-244 runs per frame. Single-threaded like the
-    reference; median of `reps` runs."""
-    import ctypes as C
+    is what src/slam.c:162-172,230-244 runs per frame. 1 core (as the
+    reference) and all cores (OpenMP over rows); median of `reps` after one
+    warm-up."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     from pyoracle import Oracle
     orc = Oracle()
-    ref_path = os.path.join(ROOT, "oracle", "_ref", "libref8x8.so")
-    if not os.path.exists(ref_path):
+    lib = _ref_lib()
+    if lib is None:
         return None
-    lib = C.CDLL(ref_path)
-    lib.buildKDTree.restype = C.c_void_p
-    lib.buildKDTree.argtypes = [C.c_void_p, C.c_size_t, C.c_int]
-    lib.freeKDTree.argtypes = [C.c_void_p]
-    fn = C.cast(lib.nearestNeighborSearch, C.c_void_p).value
-    R = src.shape[0]
-    times, nq = [], 0
-    for _ in range(reps):
-        t0 = time.perf_counter()
-        sm = orc.extract_feature(src)
-        tm = orc.extract_feature(tgt)
-        nq = 0
-        for r in range(R):
-            arr = np.ascontiguousarray(tgt[r][tm[r] == 1])
-            qs = np.ascontiguousarray(src[r][sm[r] == 1])
-            nq += len(qs)
-            root = lib.buildKDTree(arr.ctypes.data, len(arr), 0)
-            if len(arr) and len(qs):
-                orc.ref_nn_batch(fn, root, qs)
-            lib.freeKDTree(root)
-        times.append(time.perf_counter() - t0)
-    t = float(np.median(times))
-    return {"value": nq / t, "unit": "matches/s", "cores": 1, "kind": "reference",
-            "seconds_per_pair": t,
-            "sample": (f"one {src.shape[0]}x{src.shape[1]} L9-shaped pair ({nq} source-feature "
-                       f"queries), median of {reps}: extract_feature x2 + per-row buildKDTree + "
-                       "nearestNeighborSearch per source feature")}
+    fns = tuple(_addr(lib, f) for f in ("buildKDTree", "nearestNeighborSearch", "freeKDTree"))
+    nq = [0]
+
+    def run(threads):
+        def once():
+            if threads == 1:
+                sm, tm = orc.extract_feature(src), orc.extract_feature(tgt)
+            else:
+                sm, tm = orc.extract_feature_mt(src, threads), orc.extract_feature_mt(tgt, threads)
+            nq[0] = orc.ref_rows_match(fns, src, tgt, sm, tm, threads)[2]
+        return once
+
+    t1, ts1 = median_after_warmup(run(1), reps)
+    threads = orc.max_threads()
+    tall, tsall = median_after_warmup(run(threads), reps)
+    return {"value": round(nq[0] / t1, 1), "unit": "matches/s", "cores": 1, "kind": "reference",
+            "seconds_per_pair": round(t1, 5), "runs_s": [round(t, 5) for t in ts1],
+            "all_cores": {"value": round(nq[0] / tall, 1), "unit": "matches/s",
+                          "cores": threads, "seconds_per_pair": round(tall, 5),
+                          "runs_s": [round(t, 5) for t in tsall],
+                          "note": "OpenMP over rows (build + queries) and curvature rows"},
+            "host": host_info(),
+            "sample": (f"one {src.shape[0]}x{src.shape[1]} L9-shaped pair ({nq[0]} source-feature "
+                       f"queries), median of {reps} after 1 warm-up: extract_feature x2 + per-row "
+                       "buildKDTree + nearestNeighborSearch per source feature")}
 
 
 def run_k5(a, ws, rank, dev):
@@ -360,36 +426,46 @@ def main():
     if a.workload == "k3":
         R = a.rows or 512
         Cc = a.cols or 2048
-        s_seed, t_seed = shard.pair_seeds(rank)
-        src_h, tgt_h = synth.uniform_pair(R, Cc, seed_src=s_seed, seed_tgt=t_seed)
         N = R * Cc
-        src = torch.from_numpy(src_h).to(dev)
-        tgt = torch.from_numpy(tgt_h).to(dev)
-        sm = torch.empty((R, Cc), dtype=torch.int32, device=dev)
-        tm = torch.empty((R, Cc), dtype=torch.int32, device=dev)
-        idx = torch.empty((N, a.k), dtype=torch.int32, device=dev)
-        dst = torch.empty((N, a.k), dtype=torch.float64, device=dev)
-
+        # distinct pairs resident in HBM, rotated per step: pair j of rank r
+        # has seeds (1 + 2r + 1000 j, 2 + 2r + 1000 j); pair 0 is the
+        # canonical K3 pair (seeds 1, 2 on rank 0)
+        npairs = max(1, a.resident_pairs)
+        s_seed, t_seed = shard.pair_seeds(rank)
+        pairs_h = [synth.uniform_pair(R, Cc, seed_src=s_seed + 1000 * j,
+                                      seed_tgt=t_seed + 1000 * j) for j in range(npairs)]
+        src_h, tgt_h = pairs_h[0]
+        pairs_d = [(torch.from_numpy(sh).to(dev), torch.from_numpy(th).to(dev))
+                   for sh, th in pairs_h]
+        del pairs_h
         nf = max(1, a.inflight)
         # pairs in flight: context j (its own stream, workspace and outputs)
-        # takes steps j, j + nf, ...; g (context 0) is the one timed
+        # takes steps j, j + nf, ...
         extra = [NavGpu(dev.index, torch.cuda.Stream(dev).cuda_stream) for _ in range(nf - 1)]
-        outs = [(sm, tm, idx, dst)] + [tuple(torch.empty_like(t) for t in (sm, tm, idx, dst))
-                                       for _ in range(nf - 1)]
+        outs = [tuple(torch.empty(shape, dtype=dt, device=dev) for shape, dt in
+                      (((R, Cc), torch.int32), ((R, Cc), torch.int32), ((N, a.k), torch.int32),
+                       ((N, a.k), torch.float64)))
+                for _ in range(nf)]
         ctxs = [g] + extra
         turn = [0]
 
         def step():
-            j = turn[0] % nf
+            i = turn[0]
             turn[0] += 1
-            ctxs[j].pair_knn_dev(src, tgt, R, Cc, a.k, *outs[j])
+            src, tgt = pairs_d[i % npairs]
+            ctxs[i % nf].pair_knn_dev(src, tgt, R, Cc, a.k, *outs[i % nf])
+
+        def iso_step():  # one context alone: nothing else shares the chip
+            src, tgt = pairs_d[turn[0] % npairs]
+            turn[0] += 1
+            g.pair_knn_dev(src, tgt, R, Cc, a.k, *outs[0])
         if a.graph and nf == 1:
             for _ in range(2):  # warm: workspace grown, nothing allocates while capturing
                 step()
             torch.cuda.synchronize()
             graph = torch.cuda.CUDAGraph()
             with torch.cuda.graph(graph, stream=stream):
-                step()
+                g.pair_knn_dev(pairs_d[0][0], pairs_d[0][1], R, Cc, a.k, *outs[0])
             step = graph.replay  # noqa: F811
         matches_per_step = N
         dom = "knn_query"
@@ -399,10 +475,13 @@ def main():
         workload = (f"K3: {N}-point scan pair ({R}x{Cc} grid, U[0,1000)^3 mm), curvature "
                     f"on both clouds + grid index build + exact k={a.k} NN of every source "
                     "point, global mode")
-        data = "synthetic: x,y,z ~ U[0,1000) mm, numpy PCG64 seeds (1+2r, 2+2r) on rank r"
+        data = (f"synthetic: x,y,z ~ U[0,1000) mm, numpy PCG64 seeds (1+2r+1000j, 2+2r+1000j) "
+                f"on rank r, {npairs} distinct pairs j resident and rotated per step")
         cfg_extra = {"points_per_cloud": N, "k": a.k, "pairs_per_gpu": 1, "mode": "global",
-                     "pairs_in_flight": nf}
+                     "pairs_in_flight": nf, "resident_pairs": npairs,
+                     "resident_bytes": npairs * 2 * 24 * N}
     else:
+        ctxs, iso_step, nf = [g], None, 1
         R = a.rows or 128
         Cc = a.cols or 2048
         N = R * Cc
@@ -425,11 +504,15 @@ def main():
             btgt = torch.stack([tgts[p % nd] for p in range(pairs)])
         sm = torch.empty((pmax, R, Cc), dtype=torch.int32, device=dev)
         tm = torch.empty((pmax, R, Cc), dtype=torch.int32, device=dev)
-        idx = torch.full((pmax, R, Cc), -1, dtype=torch.int32, device=dev)
-        dst = torch.empty((pmax, R, Cc), dtype=torch.float64, device=dev)
+        # the rank's match sets as ONE packed buffer: idx [pmax][R][C] int32,
+        # then dist [pmax][R][C] f64 -- 12 B per grid cell, so the
+        # K4 exchange is a single all-gather
+        packed = torch.empty(pmax * N * 12, dtype=torch.uint8, device=dev)
+        idx, dst = shard.match_views(packed, pmax, R, Cc)
+        idx.fill_(-1)
         gather_buf = None
         if a.workload == "k4" and ws > 1:
-            gather_buf = torch.empty((ws * pmax, R, Cc), dtype=torch.int32, device=dev)
+            gather_buf = torch.empty(ws * packed.numel(), dtype=torch.uint8, device=dev)
 
         def step():
             if a.workload == "k4":  # one launch over the rank's whole batch
@@ -438,7 +521,7 @@ def main():
             else:
                 g.rows_match_dev(srcs[0], tgts[0], R, Cc, sm[0], tm[0], idx[0], dst[0])
             if gather_buf is not None:
-                shard.gather_matches(idx, gather_buf)
+                shard.gather_matches(packed, gather_buf)
         # matches = feature queries actually searched (constant per pair)
         step()
         torch.cuda.synchronize()
@@ -460,7 +543,8 @@ def main():
         workload = (f"{'K2' if a.workload == 'k2' else 'K4'}: {pairs} L9-shaped {R}x{Cc} "
                     "scan pair(s) per GPU, per-row mode (slam.c semantics): curvature of both "
                     "clouds + exact reference KD per target row + 1-NN of every source feature"
-                    + (", RCCL all-gather of the match sets" if gather_buf is not None else ""))
+                    + (", RCCL all-gather of the match sets (idx + dist, 12 B per cell)"
+                       if gather_buf is not None else ""))
         data = "synthetic L9-shaped range images (navslam.synth.l9_pair), fixed seeds"
         cfg_extra = {"points_per_cloud": N, "k": 1, "pairs_per_gpu": pairs, "mode": "rows"}
 
@@ -470,9 +554,28 @@ def main():
     torch.cuda.synchronize()
     if ws > 1:
         dist.barrier()
-    g.timing(True)
-    for name in set(path_kernels + [dom]):
-        g.timing_read(name, reset=True)
+    # kernel timing on every context; each kernel's average is its summed
+    # time over its own launch count (with pairs in flight, a context runs
+    # only every nf-th step)
+    names = sorted(set(path_kernels + [dom]))
+
+    def timing_on(on):
+        for c in ctxs:
+            c.timing(on)
+            for name in names:
+                c.timing_read(name, reset=True)
+
+    def timing_collect():
+        agg = {}
+        for name in names:
+            ms = n = 0
+            for c in ctxs:
+                m_, n_ = c.timing_read(name, reset=True)
+                ms += m_
+                n += n_
+            agg[name] = (ms, n)
+        return agg
+    timing_on(True)
     torch.cuda.synchronize()
     if ws > 1:
         dist.barrier()
@@ -483,13 +586,18 @@ def main():
     if ws > 1:
         dist.barrier()
     t1 = time.perf_counter()
-    g.timing(False)
     elapsed = shard.max_over_ranks(t1 - t0, dev)
     job_matches = shard.sum_over_ranks(matches_per_step, dev)
-    kt = {}
-    for name in set(path_kernels + [dom]):
-        ms, n = g.timing_read(name, reset=True)
-        kt[name] = (ms, n)
+    kt = timing_collect()
+    # isolated kernel durations: the same steps on one context alone, after
+    # the timed region (K3 with pairs in flight only)
+    kt_iso = None
+    if iso_step is not None and nf > 1 and a.iso_steps > 0:
+        for _ in range(a.iso_steps):
+            iso_step()
+        torch.cuda.synchronize()
+        kt_iso = timing_collect()
+    timing_on(False)
 
     out = None
     if rank == 0:
@@ -512,9 +620,16 @@ def main():
                     "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic,
                     "kernel": ("query stage k_knn<%d,false> + k_knn<%d,true> (overflow tiles) "
                                "+ k_knn_slow<%d>, one launch each per step" % (a.k, a.k, a.k)),
-                    "avg_us": round(dom_avg_us, 2),
+                    "avg_us": round(dom_avg_us, 2), "launches": dom_n,
+                    "timing": ("HIP events on each context's stream over the timed region"
+                               + (f" ({nf} pairs in flight: shares the chip with the other "
+                                  "pair's build)" if nf > 1 else "")),
                     "bytes_per_launch": dom_bytes,
                     "bytes_model": "24 B/query read + 24 B/target read + 12*k B/query out"}
+            if kt_iso is not None and kt_iso.get(dom, (0, 0))[1] > 0:
+                iso_us = 1000.0 * kt_iso[dom][0] / kt_iso[dom][1]
+                roof["avg_us_isolated"] = round(iso_us, 2)
+                roof["frac_isolated"] = round(dom_bytes / (iso_us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)
         elif dom_n > 0:
             roof = {"bound": "hbm", "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": None, "traffic": None, "kernel": dom,
@@ -532,14 +647,22 @@ def main():
                              "Lomuto partition passes per row (DESIGN.md)")}
         path = None
         if path_bytes is not None:
-            tot_us = 0.0
-            for kname in path_kernels:
-                ms, n = kt.get(kname, (0.0, 0))
-                tot_us += 1000.0 * ms / max(a.steps, 1)
-            if tot_us > 0:
+            def path_of(tab, label):
+                tot_us = 0.0
+                for kname in path_kernels:
+                    ms, n = tab.get(kname, (0.0, 0))
+                    if n == 0:
+                        return None
+                    tot_us += 1000.0 * ms / n   # per launch = per pair
                 pa = path_bytes / (tot_us * 1e-6) / 1e9
-                path = {"kernels_us_per_step": round(tot_us, 2), "bytes_per_step": path_bytes,
-                        "achieved": round(pa, 1), "frac": round(pa / HBM_PEAK_GBS, 4)}
+                return {"kernels_us_per_pair": round(tot_us, 2), "bytes_per_pair": path_bytes,
+                        "achieved": round(pa, 1), "frac": round(pa / HBM_PEAK_GBS, 4),
+                        "timing": label}
+            path = path_of(kt, "timed region" + (f", {nf} pairs in flight (contended)"
+                                                 if nf > 1 else ""))
+            if kt_iso is not None:
+                path = dict(path or {}, isolated=path_of(kt_iso, f"{a.iso_steps} steps on one "
+                                                        "context after the timed region"))
         cpu = None
         if ws == 1 and not a.no_cpu_baseline and a.workload == "k3":
             cpu = cpu_baseline_k3(src_h, tgt_h, a.k, a.cpu_reps)
@@ -554,6 +677,9 @@ def main():
                               **cfg_extra),
                "roofline": roof, "curvature_plus_query": path,
                "kernel_us": {k: round(1000.0 * v[0] / max(v[1], 1), 2) for k, v in kt.items()},
+               "kernel_us_isolated": (None if kt_iso is None else
+                                      {k: round(1000.0 * v[0] / max(v[1], 1), 2)
+                                       for k, v in kt_iso.items()}),
                "cpu_baseline": cpu}
         line = json.dumps(out)
         print(line, flush=True)

@@ -118,8 +118,9 @@ int navgpu_kd_query_rows_dev(navgpu_ctx *ctx, const double *tree_pts,
  * Over the output of navgpu_kd_query_rows: of the queries of row r whose
  * nearest points have equal coordinates, keep the first column at the
  * smallest distance (the reference list's final entry). keep[r*C+c] = 1 for
- * a kept correspondence (nullable); sums[r*6 .. r*6+4] = sum over kept
- * pairs of d = ori - nearest: d.x, d.y, d.z, |d|^2, count; sums[r*6+5] =
+ * a kept correspondence (nullable); sums[r*6 .. r*6+4] over the row's kept
+ * pairs of d = ori - nearest: sum d.x, d.y, d.z; sum |d - mean|^2 (centred,
+ * mean = the row's own mean of d); count; sums[r*6+5] =
  * the row's queries that found a nearest point. Order-free: used
  * by the shim's closed-form Adam (NAVSLAM_ADAM=fast); the bit-exact mode
  * keeps the reference's sequential list on the host. */

@@ -999,7 +999,8 @@ inline int kd_build_lds_bytes(int n) {
 // per-point minimum is two LDS atomicMin passes (distance bits, then
 // column). Outputs: keep[r*C+c] (1 = kept correspondence; nullable) and the
 // row's residual sums over kept pairs, d = ori - near:
-//   sums[r*6 + {0,1,2}] = sum d.x, d.y, d.z; [3] = sum |d|^2; [4] = count;
+//   sums[r*6 + {0,1,2}] = sum d.x, d.y, d.z; [3] = sum |d - mean d|^2 (the
+//   centred second moment, mean over the row's kept pairs); [4] = count;
 //   [5] = queries of the row that found a nearest point (before the dedup).
 // Order-free: the sums are what a closed-form Adam step needs (the
 // reference's own sequential sum order is kept by the host path instead).
@@ -1081,26 +1082,47 @@ __global__ __launch_bounds__(kCorrBlock) void k_rows_corr(
     if (keep) keep[base + c] = kept ? 1 : 0;
     if (kept) {
       const double *a = ori + 3 * (base + c), *b = tree_pts + 3 * (base + pos);
-      const double dx = a[0] - b[0], dy = a[1] - b[1], dz = a[2] - b[2];
-      acc[0] += dx;
-      acc[1] += dy;
-      acc[2] += dz;
-      acc[3] += dx * dx + dy * dy + dz * dz;
+      acc[0] += a[0] - b[0];
+      acc[1] += a[1] - b[1];
+      acc[2] += a[2] - b[2];
       acc[4] += 1.0;
     }
   }
-#pragma unroll
-  for (int k = 0; k < 6; ++k)
-    for (int o = kWave / 2; o > 0; o >>= 1) acc[k] += __shfl_xor(acc[k], o, kWave);
-  if ((threadIdx.x & (kWave - 1)) == 0)
-#pragma unroll
-    for (int k = 0; k < 6; ++k) red[threadIdx.x / kWave][k] = acc[k];
-  __syncthreads();
-  if (threadIdx.x < 6) {
-    double t = 0.0;
-    for (int w = 0; w < kCorrBlock / kWave; ++w) t += red[w][threadIdx.x];
-    sums[(size_t)row * 6 + threadIdx.x] = t;
+  auto block_sum = [&](double *v, int nv) {  // every thread gets the block totals
+#pragma unroll 1
+    for (int k = 0; k < nv; ++k)
+      for (int o = kWave / 2; o > 0; o >>= 1) v[k] += __shfl_xor(v[k], o, kWave);
+    __syncthreads();
+    if ((threadIdx.x & (kWave - 1)) == 0)
+      for (int k = 0; k < nv; ++k) red[threadIdx.x / kWave][k] = v[k];
+    __syncthreads();
+    for (int k = 0; k < nv; ++k) {
+      double t = 0.0;
+      for (int w = 0; w < kCorrBlock / kWave; ++w) t += red[w][k];
+      v[k] = t;
+    }
+  };
+  block_sum(acc, 6);
+  // second pass: the centred second moment sum |d - mean|^2. E(t) =
+  // M2 + n |mean - t|^2 then keeps its significant digits when the residuals
+  // are small against d itself (the uncentred sum |d|^2 - 2 t.S1 + n|t|^2
+  // cancels catastrophically, and can even go negative).
+  const double cnt = acc[4];
+  const double mx = cnt > 0 ? acc[0] / cnt : 0.0, my = cnt > 0 ? acc[1] / cnt : 0.0,
+               mz = cnt > 0 ? acc[2] / cnt : 0.0;
+  double m2 = 0.0;
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+    const int pos = nn_pos[base + c];
+    if (pos < 0 || pos >= n) continue;
+    const int h = canon[pos];
+    if (!(h < 0 || bcol[h] == c)) continue;
+    const double *a = ori + 3 * (base + c), *b = tree_pts + 3 * (base + pos);
+    const double ex = (a[0] - b[0]) - mx, ey = (a[1] - b[1]) - my, ez = (a[2] - b[2]) - mz;
+    m2 += ex * ex + ey * ey + ez * ez;
   }
+  block_sum(&m2, 1);
+  if (threadIdx.x < 6)
+    sums[(size_t)row * 6 + threadIdx.x] = threadIdx.x == 3 ? m2 : acc[threadIdx.x];
 }
 
 // ============================================================ global mode

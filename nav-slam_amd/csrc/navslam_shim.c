@@ -397,10 +397,12 @@ static uint64_t hash3(const double *p)
 
 /* The NAVSLAM_ADAM=fast tail of slam_localization: dedup + residual sums on
  * the GPU (navgpu_rows_corr_dev), then src/slam.c:300-389's Adam loop with
- * every per-iteration sum in closed form. With d_i = ori_i - near_i and
- * dx_i = (ori_i - t) - near_i = d_i - t:
- *   sum dx = S1 - n t,   totalError = sum |d_i - t|^2 = S2 - 2 t.S1 + n |t|^2
- * (exact in real arithmetic; rounding differs from the sequential sums). */
+ * every per-iteration sum in closed form. With d_i = ori_i - near_i, its
+ * mean m and dx_i = (ori_i - t) - near_i = d_i - t:
+ *   sum dx = n (m - t),   totalError = sum |d_i - t|^2 = M2 + n |m - t|^2
+ * where M2 = sum |d_i - m|^2 comes centred from the GPU (per row, merged
+ * here), so no cancellation and never negative (exact in real arithmetic;
+ * rounding differs from the reference's sequential sums). */
 static Pos localization_fast(SLAM_attr *attr, slam_state *s, double transform[6],
                              Pos pos_last)
 {
@@ -409,15 +411,24 @@ static Pos localization_fast(SLAM_attr *attr, slam_state *s, double transform[6]
                             ROWS, COLS, NULL, s->d_sums));
     CK(navgpu_download(c, s->h_sums, s->d_sums, sizeof(s->h_sums)));
     CK(navgpu_sync(c));
-    double S1[3] = {0.0, 0.0, 0.0}, S2 = 0.0, n = 0.0, nq = 0.0;
+    /* merge the rows' (count, mean, centred M2) with Chan et al.'s pairwise
+     * update: M2 = M2a + M2b + |mb - ma|^2 na nb / (na + nb) */
+    double mean[3] = {0.0, 0.0, 0.0}, M2 = 0.0, n = 0.0, nq = 0.0;
     for (int r = 0; r < ROWS; r++) {
         const double *h = s->h_sums + 6 * r;
-        S1[0] += h[0];
-        S1[1] += h[1];
-        S1[2] += h[2];
-        S2 += h[3];
-        n += h[4];
         nq += h[5];
+        const double nb = h[4];
+        if (!(nb > 0))
+            continue;
+        const double tot = n + nb;
+        double dm[3], dd = 0.0;
+        for (int j = 0; j < 3; j++) {
+            dm[j] = h[j] / nb - mean[j];
+            dd += dm[j] * dm[j];
+            mean[j] += dm[j] * (nb / tot);
+        }
+        M2 += h[3] + dd * (n * nb / tot);
+        n = tot;
     }
     double learningRate = 0.1, tolerance = 1e-6;
     double previousTotalError = 0, totalError = 0;
@@ -428,10 +439,14 @@ static Pos localization_fast(SLAM_attr *attr, slam_state *s, double transform[6]
     for (iter = 0; iter < 200; ++iter) {
         const double *t = transform;
         double gradient[3];
-        for (int j = 0; j < 3; j++)
-            gradient[j] = -(S1[j] - n * t[j]);
-        totalError = S2 - 2.0 * (t[0] * S1[0] + t[1] * S1[1] + t[2] * S1[2]) +
-                     n * (t[0] * t[0] + t[1] * t[1] + t[2] * t[2]);
+        /* sum dx_i = n (mean - t); sum |dx_i|^2 = M2 + n |mean - t|^2 >= 0 */
+        double off2 = 0.0;
+        for (int j = 0; j < 3; j++) {
+            const double e = mean[j] - t[j];
+            gradient[j] = -(n * e);
+            off2 += e * e;
+        }
+        totalError = M2 + n * off2;
         if (fabs(totalError - previousTotalError) < tolerance) {
             if (!q)
                 printf("\xe6\x94\xb6\xe6\x95\x9b\xef\xbc\x8c\xe5\x81\x9c\xe6\xad\xa2"

@@ -42,10 +42,33 @@ def sum_over_ranks(value, device):
     return float(t.item())
 
 
+def match_views(packed, pairs, R, C):
+    """The K4 match set of `pairs` pairs as one packed byte buffer of
+    pairs * R * C * 12 bytes: nn_idx [pairs][R][C] int32 first, then nn_dist
+    [pairs][R][C] float64 (idx + dist, 12 B per match). Returns the
+    (idx, dist) views the kernels write into."""
+    n = pairs * R * C
+    if packed.numel() != 12 * n or packed.dtype != torch.uint8:
+        raise ValueError("packed match buffer must be uint8[pairs*R*C*12]")
+    idx = packed[: 4 * n].view(torch.int32).view(pairs, R, C)
+    dist = packed[4 * n:].view(torch.float64).view(pairs, R, C)
+    return idx, dist
+
+
+def unpack_gathered(gathered, world, pairs, R, C):
+    """Rank-ordered (idx [world*pairs][R][C], dist [world*pairs][R][C]) from
+    the all-gathered packed buffers."""
+    parts = gathered.view(world, -1)
+    idx = torch.cat([match_views(parts[w], pairs, R, C)[0] for w in range(world)])
+    dist = torch.cat([match_views(parts[w], pairs, R, C)[1] for w in range(world)])
+    return idx, dist
+
+
 def gather_matches(local, out=None):
     """All-gather the per-pair match buffers of every rank, in rank order:
     local [p, ...] -> [world * p, ...]. Every rank must hold the same p (K4
-    sizes the shards so; a ragged tail is padded by the caller)."""
+    sizes the shards so: ceil(total / world) slots per rank, the ragged
+    tail's unused slots padded by the caller)."""
     world = dist.get_world_size()
     if out is None:
         out = torch.empty((world * local.shape[0],) + tuple(local.shape[1:]),

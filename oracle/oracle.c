@@ -407,6 +407,82 @@ typedef struct {
     double ori[3], near[3], dist;
 } orc_corr;
 
+/* src/slam.c:236-284: the correspondence list of one frame, built row by row
+ * from the per-feature 1-NN results (pos[g] = tree position in row g / C, -1
+ * for a non-feature or an empty row tree; dist[g] its distance). Within a
+ * row, a nearest point equal in x, y and z (==) to an entry already listed
+ * for that row replaces the entry only when strictly closer; otherwise it is
+ * appended. `col` (nullable) receives the grid index of each entry's
+ * current query. Returns CPcount. */
+static int orc_dedup_list(const double *trees, int R, int C, const long *pos,
+                          const double *dist, const double *tp, orc_corr *res, long *col)
+{
+    int CPcount = 0, flag = 0;
+    for (int row = 0; row < R; ++row) {
+        const double *tree = trees + 3 * (size_t)row * C;
+        for (int col_ = 0; col_ < C; ++col_) {
+            size_t g = (size_t)row * C + col_;
+            /* Empty row tree: the reference reads an uninitialised Point
+             * (slam.c:242-252, undefined behaviour); here the query makes no
+             * correspondence. */
+            if (pos[g] < 0)
+                continue;
+            const double *np = tree + 3 * pos[g];
+            double bestDist = dist[g];
+            if (flag == CPcount) {
+                memcpy(res[CPcount].ori, tp + 3 * g, 24);
+                memcpy(res[CPcount].near, np, 24);
+                res[CPcount].dist = bestDist;
+                if (col)
+                    col[CPcount] = (long)g;
+                CPcount++;
+                continue;
+            }
+            int found = 0;
+            for (int i = flag; i < CPcount; i++) {
+                if (res[i].near[0] == np[0] && res[i].near[1] == np[1] &&
+                    res[i].near[2] == np[2]) {
+                    if (res[i].dist > bestDist) {
+                        memcpy(res[i].ori, tp + 3 * g, 24);
+                        memcpy(res[i].near, np, 24);
+                        res[i].dist = bestDist;
+                        if (col)
+                            col[i] = (long)g;
+                    }
+                    found = 1;
+                    break;
+                }
+            }
+            if (!found) {
+                memcpy(res[CPcount].ori, tp + 3 * g, 24);
+                memcpy(res[CPcount].near, np, 24);
+                res[CPcount].dist = bestDist;
+                if (col)
+                    col[CPcount] = (long)g;
+                CPcount++;
+            }
+        }
+        flag = CPcount;
+    }
+    return CPcount;
+}
+
+int orc_rows_dedup(const double *trees, int R, int C, const long *pos, const double *dist,
+                   const double *ori, double *out_ori, double *out_near, double *out_dist,
+                   long *out_grid)
+{
+    size_t N = (size_t)R * C;
+    orc_corr *res = malloc(sizeof(orc_corr) * (N ? N : 1));
+    int n = orc_dedup_list(trees, R, C, pos, dist, ori, res, out_grid);
+    for (int i = 0; i < n; i++) {
+        memcpy(out_ori + 3 * (size_t)i, res[i].ori, 24);
+        memcpy(out_near + 3 * (size_t)i, res[i].near, 24);
+        out_dist[i] = res[i].dist;
+    }
+    free(res);
+    return n;
+}
+
 void orc_slam_localization(orc_slam *s, const double *lidar,
                            const double pred[6], const double last[6],
                            double out[6], int *iters_out, int *ncorr_out)
@@ -426,6 +502,8 @@ void orc_slam_localization(orc_slam *s, const double *lidar,
     orc_map_to_last(tp, N, transform, ql);
 
     orc_corr *res = malloc(sizeof(orc_corr) * (N ? N : 1));
+    long *pos = malloc(sizeof(long) * (N ? N : 1));
+    double *bd = malloc(sizeof(double) * (N ? N : 1));
     int CPcount = 0;
     double learningRate = 0.1, tolerance = 1e-6;
     double previousTotalError = 0, totalError = 0;
@@ -435,51 +513,15 @@ void orc_slam_localization(orc_slam *s, const double *lidar,
     int iter;
     for (iter = 0; iter < 200; ++iter) {
         if (iter % 200 == 0) { /* slam.c:233-284 */
-            int flag = 0;
-            for (int row = 0; row < R; ++row) {
-                const double *tree = s->tree + 3 * (size_t)row * C;
+            for (int row = 0; row < R; ++row)
                 for (int col = 0; col < C; ++col) {
                     size_t g = (size_t)row * C + col;
-                    if (feature[g] != 1)
-                        continue;
-                    long pos;
-                    double bestDist;
-                    orc_kd_nn(tree, s->tn[row], ql + 3 * g, &pos, &bestDist);
-                    /* Empty row tree: the reference reads an uninitialised
-                     * Point (slam.c:242-252, undefined behaviour); here the
-                     * query makes no correspondence. */
-                    if (pos < 0)
-                        continue;
-                    const double *np = tree + 3 * pos;
-                    if (flag == CPcount) {
-                        memcpy(res[CPcount].ori, tp + 3 * g, 24);
-                        memcpy(res[CPcount].near, np, 24);
-                        res[CPcount].dist = bestDist;
-                        CPcount++;
-                        continue;
-                    }
-                    int found = 0;
-                    for (int i = flag; i < CPcount; i++) {
-                        if (res[i].near[0] == np[0] && res[i].near[1] == np[1] &&
-                            res[i].near[2] == np[2]) {
-                            if (res[i].dist > bestDist) {
-                                memcpy(res[i].ori, tp + 3 * g, 24);
-                                memcpy(res[i].near, np, 24);
-                                res[i].dist = bestDist;
-                            }
-                            found = 1;
-                            break;
-                        }
-                    }
-                    if (!found) {
-                        memcpy(res[CPcount].ori, tp + 3 * g, 24);
-                        memcpy(res[CPcount].near, np, 24);
-                        res[CPcount].dist = bestDist;
-                        CPcount++;
-                    }
+                    pos[g] = -1;
+                    if (feature[g] == 1)
+                        orc_kd_nn(s->tree + 3 * (size_t)row * C, s->tn[row], ql + 3 * g,
+                                  &pos[g], &bd[g]);
                 }
-                flag = CPcount;
-            }
+            CPcount = orc_dedup_list(s->tree, R, C, pos, bd, tp, res, NULL);
         }
         /* slam.c:318-373 (ErrDistance, slam.c:301-308, has no effect) */
         double gradient[3] = {0.0, 0.0, 0.0};
@@ -527,6 +569,8 @@ void orc_slam_localization(orc_slam *s, const double *lidar,
     free(tp);
     free(ql);
     free(res);
+    free(pos);
+    free(bd);
 }
 
 double orc_slam_error(const orc_slam *s) { return s->error; }

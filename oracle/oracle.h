@@ -100,6 +100,35 @@ void orc_kd_nn_batch(const double *tree, size_t n, const double *qs, size_t nq,
 void orc_ref_nn_batch(void *fn, void *root, const double *qs, size_t nq,
                       double *out_pts, double *out_dist);
 
+/* oracle_grid.c: the same k-NN as orc_knn_brute (identical results, pinned
+ * by tests/test_oracle.py) over a uniform grid searched in growing shells,
+ * OpenMP over the queries: checks all 1M K3 queries in seconds. */
+void orc_knn_grid(const double *tgt, size_t nt, const double *qs, size_t nq,
+                  int k, int *out_idx, double *out_dist);
+
+/* oracle_grid.c: all-cores CPU-baseline drivers (OpenMP). The reference's
+ * own buildKDTree / nearestNeighborSearch / freeKDTree are passed in as
+ * function pointers (oracle/_ref build). */
+void orc_ref_nn_batch_mt(void *fn, void *root, const double *qs, size_t nq,
+                         double *out_pts, double *out_dist);
+long orc_ref_rows_match_mt(void *build, void *nn, void *freef,
+                           const double *src, const double *tgt,
+                           const int *smask, const int *tmask, int R, int C,
+                           int threads, double *out_pts, double *out_dist);
+void orc_extract_feature_mt(const double *pts, int R, int C, int *feature,
+                            int threads);
+int orc_max_threads(void);
+
+/* src/slam.c:236-284: a frame's correspondence list from per-feature 1-NN
+ * results over per-row trees (trees: row r's tree at offset r*C; pos[g]: tree
+ * position, -1 = no query/empty tree; dist[g]; ori[g]: the query's
+ * transformed point). Writes the list in the reference's order: ori, nearest
+ * point, distance and the grid index g of each entry's query. Returns the
+ * entry count (CPcount). The same code orc_slam_localization runs. */
+int orc_rows_dedup(const double *trees, int R, int C, const long *pos,
+                   const double *dist, const double *ori, double *out_ori,
+                   double *out_near, double *out_dist, long *out_grid);
+
 /* ---- src/slam.c:134-431 frame loop, runtime dims, buffers sized R*C ---- */
 typedef struct orc_slam orc_slam;
 orc_slam *orc_slam_create(int R, int C);

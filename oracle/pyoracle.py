@@ -45,6 +45,16 @@ class Oracle:
         L.orc_kd_nn_batch.argtypes = [_dp, C.c_size_t, _dp, C.c_size_t,
                                       C.POINTER(C.c_long), _dp]
         L.orc_ref_nn_batch.argtypes = [C.c_void_p, C.c_void_p, _dp, C.c_size_t, _dp, _dp]
+        L.orc_knn_grid.argtypes = [_dp, C.c_size_t, _dp, C.c_size_t, C.c_int, _ip, _dp]
+        L.orc_ref_nn_batch_mt.argtypes = [C.c_void_p, C.c_void_p, _dp, C.c_size_t, _dp, _dp]
+        L.orc_ref_rows_match_mt.restype = C.c_long
+        L.orc_ref_rows_match_mt.argtypes = [C.c_void_p] * 3 + [_dp, _dp, _ip, _ip, C.c_int,
+                                                               C.c_int, C.c_int, _dp, _dp]
+        L.orc_extract_feature_mt.argtypes = [_dp, C.c_int, C.c_int, _ip, C.c_int]
+        L.orc_max_threads.restype = C.c_int
+        L.orc_rows_dedup.restype = C.c_int
+        L.orc_rows_dedup.argtypes = [_dp, C.c_int, C.c_int, C.c_void_p, _dp, _dp, _dp, _dp, _dp,
+                                     C.c_void_p]
         L.orc_slam_create.restype = C.c_void_p
         L.orc_slam_create.argtypes = [C.c_int, C.c_int]
         L.orc_slam_destroy.argtypes = [C.c_void_p]
@@ -142,6 +152,65 @@ class Oracle:
         dist = np.zeros((len(qs), k))
         self.L.orc_knn_brute(_d(tgt), len(tgt), _d(qs), len(qs), k, _i(idx), _d(dist))
         return idx, dist
+
+
+    def knn_grid(self, tgt, qs, k):
+        """Same result as knn_brute (pinned by tests/test_oracle.py), grid +
+        OpenMP: fast enough for every query of the 1M K3 pair."""
+        tgt = np.ascontiguousarray(tgt, np.float64).reshape(-1, 3)
+        qs = np.ascontiguousarray(qs, np.float64).reshape(-1, 3)
+        idx = np.zeros((len(qs), k), np.int32)
+        dist = np.zeros((len(qs), k))
+        self.L.orc_knn_grid(_d(tgt), len(tgt), _d(qs), len(qs), k, _i(idx), _d(dist))
+        return idx, dist
+
+    def ref_nn_batch_mt(self, fn_addr, root, qs):
+        qs = np.ascontiguousarray(qs, np.float64).reshape(-1, 3)
+        pts = np.zeros_like(qs)
+        d = np.zeros(len(qs))
+        self.L.orc_ref_nn_batch_mt(fn_addr, root, _d(qs), len(qs), _d(pts), _d(d))
+        return pts, d
+
+    def extract_feature_mt(self, pts, threads):
+        pts = np.ascontiguousarray(pts, np.float64)
+        R, Cc = pts.shape[:2]
+        mask = np.zeros((R, Cc), np.int32)
+        self.L.orc_extract_feature_mt(_d(pts), R, Cc, _i(mask), threads)
+        return mask
+
+    def ref_rows_match(self, fns, src, tgt, smask, tmask, threads):
+        """Per-row build + 1-NN through the reference's own functions
+        fns = (buildKDTree, nearestNeighborSearch, freeKDTree) addresses.
+        Returns (nearest points [R,C,3], distances [R,C] (+inf where no
+        query), number of queries)."""
+        src = np.ascontiguousarray(src, np.float64)
+        tgt = np.ascontiguousarray(tgt, np.float64)
+        R, Cc = src.shape[:2]
+        pts = np.zeros_like(src)
+        d = np.full((R, Cc), np.inf)
+        sm = np.ascontiguousarray(smask, np.int32)
+        tm = np.ascontiguousarray(tmask, np.int32)
+        n = self.L.orc_ref_rows_match_mt(fns[0], fns[1], fns[2], _d(src), _d(tgt), _i(sm),
+                                         _i(tm), R, Cc, threads, _d(pts), _d(d))
+        return pts, d, int(n)
+
+    def rows_dedup(self, trees, pos, dist, ori):
+        """src/slam.c:236-284 over per-row trees [R,C,3] and per-cell 1-NN
+        results pos/dist [R,C]: (ori [n,3], near [n,3], dist [n], grid index
+        [n]) in the reference list's order."""
+        trees = np.ascontiguousarray(trees, np.float64)
+        R, Cc = trees.shape[:2]
+        pos = np.ascontiguousarray(pos, np.int64)
+        dist = np.ascontiguousarray(dist, np.float64)
+        ori = np.ascontiguousarray(ori, np.float64)
+        N = R * Cc
+        o, nr, d, g = np.zeros((N, 3)), np.zeros((N, 3)), np.zeros(N), np.zeros(N, np.int64)
+        n = self.L.orc_rows_dedup(_d(trees), R, Cc, pos.ctypes.data, _d(dist), _d(ori), _d(o),
+                                  _d(nr), _d(d), g.ctypes.data)
+        return o[:n], nr[:n], d[:n], g[:n]
+
+    def max_threads(self):
+        return int(self.L.orc_max_threads())
 
 
 class OracleSlam:

@@ -16,6 +16,12 @@ inputs and stores inputs + reference outputs as .npz (no pickles):
   rows_l9.npz     per-row matching at the L9 grid (54x42): masks from the
                   oracle restatement (pinned by curv8x8), row trees and 1-NN
                   from the reference kdtree.c
+  digests.npz     SHA-256 digests at the benchmark sizes: the
+                  reference buildKDTree + nearestNeighborSearch over the 1M K3
+                  pair (k = 1), and the per-row reference search over the K2
+                  128x2048 pair (f64 and integer-mm); the inputs' own digests
+                  too, so a test can tell a different input from a different
+                  answer. `python make_golden.py digests` regenerates only it.
 
 Only this script touches the reference build; the fixtures are data.
 Usage: python tests/golden/make_golden.py   (needs oracle/_ref built)
@@ -330,7 +336,57 @@ def make_rows_l9(lib, rng):
     print("rows_l9: queries", int(out["smask_f"].sum() + out["smask_i"].sum()))
 
 
+def sha(a):
+    import hashlib
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+
+def nn_digest_arrays(tgt_flat, nn_idx, nn_dist):
+    """The arrays the digests cover: the nearest point's coordinates (0 where
+    no neighbour) and the distance (+inf where none), as float64."""
+    pts = np.zeros((len(nn_idx), 3))
+    ok = nn_idx >= 0
+    pts[ok] = tgt_flat[nn_idx[ok]]
+    return pts, np.asarray(nn_dist, np.float64)
+
+
+def make_digests(lib):
+    from navslam import synth
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    from pyoracle import Oracle
+    orc = Oracle()
+    out = {}
+    # K3: 1M-point pair, the reference's global KD 1-NN (utils/kdtree.c:65-82,110-152)
+    src, tgt = synth.uniform_pair(512, 2048)
+    N = src.shape[0] * src.shape[1]
+    arr = np.ascontiguousarray(tgt.reshape(-1, 3)).copy()
+    root = lib.buildKDTree(arr.ctypes.data_as(C.POINTER(Point)), N, 0)
+    fn = C.cast(lib.nearestNeighborSearch, C.c_void_p).value
+    pts, d = orc.ref_nn_batch(fn, C.cast(root, C.c_void_p).value, src.reshape(-1, 3))
+    lib.freeKDTree(root)
+    out.update(k3_src=sha(src), k3_tgt=sha(tgt), k3_nn=sha(pts), k3_nnd=sha(d),
+               k3_head_nn=pts[:64], k3_head_nnd=d[:64])
+    # K2: 128x2048 L9-shaped pairs, per-row reference search (src/slam.c:162-172,236-244)
+    fns = tuple(C.cast(getattr(lib, f), C.c_void_p).value
+                for f in ("buildKDTree", "nearestNeighborSearch", "freeKDTree"))
+    for tag, integer in (("f", False), ("i", True)):
+        src, tgt = synth.l9_pair(128, 2048, seed=5, integer_mm=integer)
+        sm, tm = orc.extract_feature(src), orc.extract_feature(tgt)
+        pts, d, nq = orc.ref_rows_match(fns, src, tgt, sm, tm, 1)
+        q = sm.reshape(-1) == 1
+        out.update({f"k2{tag}_src": sha(src), f"k2{tag}_tgt": sha(tgt),
+                    f"k2{tag}_smask": sha(sm), f"k2{tag}_tmask": sha(tm),
+                    f"k2{tag}_nn": sha(pts.reshape(-1, 3)[q]), f"k2{tag}_nnd": sha(d.reshape(-1)[q]),
+                    f"k2{tag}_nq": np.int64(nq)})
+        print(f"digests k2{tag}: {nq} queries")
+    np.savez_compressed(os.path.join(HERE, "digests.npz"), **out)
+    print("digests: k3", out["k3_nn"][:16])
+
+
 def main():
+    if sys.argv[1:] == ["digests"]:
+        make_digests(load_ref())
+        return
     lib = load_ref()
     rng = np.random.default_rng(20261015)
     make_curv(lib, rng)
@@ -338,6 +394,7 @@ def main():
     make_kdtree(lib, rng)
     make_slam(lib, rng)
     make_rows_l9(lib, rng)
+    make_digests(lib)
 
 
 if __name__ == "__main__":

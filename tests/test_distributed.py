@@ -43,26 +43,46 @@ def _worker(rank, world, port, pairs, R, Cc, q):
         from pyoracle import Oracle
         orc = Oracle()
         lo, hi = shard.shard_pairs(pairs, world, rank)
-        local = np.zeros((hi - lo, R, Cc), np.int32)
+        pmax = -(-pairs // world)
+        # the rank's match sets packed as bench.py's K4 does: idx then dist,
+        # 12 B per cell, pmax slots (a ragged tail leaves the last slot unused)
+        packed = torch.zeros(pmax * R * Cc * 12, dtype=torch.uint8)
+        idx, dst = shard.match_views(packed, pmax, R, Cc)
+        idx.fill_(-1)
         for i, p in enumerate(range(lo, hi)):
             src, tgt = synth.l9_pair(R, Cc, seed=100 + p, integer_mm=True)
-            local[i] = orc.rows_match(src, tgt)[2]
-        out = shard.gather_matches(torch.from_numpy(local))
+            _, _, ni, nd = orc.rows_match(src, tgt)
+            idx[i] = torch.from_numpy(ni)
+            dst[i] = torch.from_numpy(nd)
+        out = shard.gather_matches(packed)
+        gi, gd = shard.unpack_gathered(out, world, pmax, R, Cc)
         slowest = shard.max_over_ranks(0.25 * (rank + 1), torch.device("cpu"))
         total = shard.sum_over_ranks(hi - lo, torch.device("cpu"))
         if rank == 0:
-            q.put((out.numpy(), slowest, total))
+            q.put((gi.numpy(), gd.numpy(), slowest, total))
     finally:
         dist.destroy_process_group()
 
 
-def test_k4_shard_and_gather_gloo_world2(orc):
-    world, pairs, R, Cc = 2, 4, 6, 64
+@pytest.mark.parametrize("pairs", [4, 5])
+def test_k4_shard_and_gather_gloo_world2(orc, pairs):
+    """K4 plumbing at world 2 (gloo): contiguous shards, one all-gather of the
+    packed idx + dist match sets, a ragged tail (5 pairs over 2 ranks) padded;
+    the gathered sets equal a single-process run pair by pair."""
+    world, R, Cc = 2, 6, 64
     q = mp.get_context("spawn").SimpleQueue()
     mp.spawn(_worker, args=(world, _free_port(), pairs, R, Cc, q), nprocs=world, join=True)
-    gathered, slowest, total = q.get()
+    gi, gd, slowest, total = q.get()
     assert slowest == 0.5 and total == pairs
-    ref = np.stack([orc.rows_match(*synth.l9_pair(R, Cc, seed=100 + p, integer_mm=True))[2]
-                    for p in range(pairs)])
-    assert gathered.shape == ref.shape
-    assert np.array_equal(gathered, ref)
+    pmax = -(-pairs // world)
+    assert gi.shape == (world * pmax, R, Cc)
+    for p in range(pairs):
+        r = 0 if p < pmax else 1
+        slot = r * pmax + (p - shard.shard_pairs(pairs, world, r)[0])
+        _, _, ni, nd = orc.rows_match(*synth.l9_pair(R, Cc, seed=100 + p, integer_mm=True))
+        np.testing.assert_array_equal(gi[slot], ni)
+        np.testing.assert_array_equal(gd[slot], nd)
+    used = {r * pmax + i for r in range(world)
+            for i in range(np.subtract(*shard.shard_pairs(pairs, world, r)[::-1]))}
+    for slot in set(range(world * pmax)) - used:   # padding of the ragged tail
+        assert (gi[slot] == -1).all()

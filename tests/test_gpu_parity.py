@@ -298,25 +298,73 @@ def test_knn_k1_agrees_with_reference_kd_distances(gpu, golden):
         _eq(gd[:, 0], nnd, "1-NN distance vs reference KD")
 
 
-def test_knn_k3_full_size_sampled(gpu, orc):
-    """K3 at full size (1M x 1M, k=8): every query computed on the GPU, a
-    seeded sample of 1024 checked against brute force over all 1M targets;
-    size-independent properties on all queries."""
+def test_knn_k3_full_size_all_queries(gpu, orc):
+    """K3 at full size (1M x 1M, k=8): EVERY query against the oracle's exact
+    grid k-NN (orc_knn_grid, pinned to the brute force by test_oracle.py),
+    plus a seeded sample of 1024 against the brute force itself."""
     from navslam.synth import uniform_pair
     src, tgt = uniform_pair(512, 2048)
     gi, gd = gpu.knn(tgt, src, 8)
-    assert (gi >= 0).all() and np.isfinite(gd).all()
-    assert (np.diff(gd, axis=1) >= 0).all()                # sorted by distance
-    flat = tgt.reshape(-1, 3)
+    ri, rd = orc.knn_grid(tgt, src, 8)
+    _eq(gi, ri, "all 1M queries: idx")
+    _eq(gd, rd, "all 1M queries: dist")
     s = np.random.default_rng(9).choice(len(gi), 1024, replace=False)
-    ri, rd = orc.knn_brute(tgt, src.reshape(-1, 3)[s], 8)
-    _eq(gi[s], ri, "sampled idx")
-    _eq(gd[s], rd, "sampled dist")
-    # distances recomputed from the returned indices (reference formula)
-    q = src.reshape(-1, 3)
-    d = flat[gi] - q[:, None, :]
-    rec = np.sqrt(d[..., 0] * d[..., 0] + d[..., 1] * d[..., 1] + d[..., 2] * d[..., 2])
-    _eq(gd, rec, "distance of returned index")
+    bi, bd = orc.knn_brute(tgt, src.reshape(-1, 3)[s], 8)
+    _eq(gi[s], bi, "sampled idx vs brute force")
+    _eq(gd[s], bd, "sampled dist vs brute force")
+
+
+def _digest_inputs_match(dg, prefix, src, tgt):
+    from golden.make_golden import sha
+    if sha(src) != str(dg[prefix + "_src"]) or sha(tgt) != str(dg[prefix + "_tgt"]):
+        pytest.fail(f"{prefix}: the synthetic input differs from the one the reference "
+                    "digests were made from (numpy on this host generates other values)")
+
+
+def test_knn_k1_1m_matches_reference_kd_digest(gpu, golden):
+    """the reference's own buildKDTree + nearestNeighborSearch over
+    the 1M K3 pair (oracle/_ref, digests made by tests/golden/make_golden.py):
+    the GPU's 1-NN points and distances hash to the same SHA-256."""
+    from golden.make_golden import nn_digest_arrays, sha
+    from navslam.synth import uniform_pair
+    dg = golden("digests")
+    src, tgt = uniform_pair(512, 2048)
+    _digest_inputs_match(dg, "k3", src, tgt)
+    gi, gd = gpu.knn(tgt, src, 1)
+    pts, d = nn_digest_arrays(tgt.reshape(-1, 3), gi[:, 0], gd[:, 0])
+    _eq(pts[:64], dg["k3_head_nn"], "first 64 nearest points")
+    _eq(d[:64], dg["k3_head_nnd"], "first 64 distances")
+    assert sha(pts) == str(dg["k3_nn"]), "1M nearest points differ from the reference KD"
+    assert sha(d) == str(dg["k3_nnd"]), "1M distances differ from the reference KD"
+
+
+@pytest.mark.parametrize("tag,integer", [("f", False), ("i", True)])
+def test_rows_match_k2_matches_reference_digest(gpu, golden, tag, integer):
+    """the K2 128x2048 pair in per-row mode against the reference's
+    per-row buildKDTree + nearestNeighborSearch (digests of the nearest
+    points and distances of every source feature, row-major)."""
+    from golden.make_golden import nn_digest_arrays, sha
+    from navslam.synth import l9_pair
+    dg = golden("digests")
+    src, tgt = l9_pair(128, 2048, seed=5, integer_mm=integer)
+    _digest_inputs_match(dg, "k2" + tag, src, tgt)
+    sm, tm, idx, dist = gpu.rows_match(src, tgt)
+    assert sha(sm) == str(dg[f"k2{tag}_smask"]) and sha(tm) == str(dg[f"k2{tag}_tmask"])
+    q = sm.reshape(-1) == 1
+    assert int(q.sum()) == int(dg[f"k2{tag}_nq"])
+    pts, d = nn_digest_arrays(tgt.reshape(-1, 3), idx.reshape(-1)[q], dist.reshape(-1)[q])
+    assert sha(pts) == str(dg[f"k2{tag}_nn"]), "nearest points differ from the reference"
+    assert sha(d) == str(dg[f"k2{tag}_nnd"]), "distances differ from the reference"
+
+
+def test_curvature_k3_shape_bit_exact(gpu, orc):
+    """R1 at the K3 shape: both 512x2048 clouds, mask and f64 value."""
+    from navslam.synth import uniform_pair
+    for pts in uniform_pair(512, 2048):
+        m_ref, c_ref = orc.extract_feature(pts, want_curv=True)
+        m, cv = gpu.curvature(pts, want_curv=True)
+        _eq(m, m_ref, "512x2048 mask")
+        _eq(cv, c_ref, "512x2048 curvature")
 
 
 # ------------------------------------------------------- slam.h drop-in
@@ -452,41 +500,30 @@ def test_shim_l9_stream_vs_oracle(monkeypatch, R, Cc, F, steps):
     assert attr.frameCount == s.frame_count
 
 
-def _dedup_reference(tree, tn, pos, dist, ori):
-    """src/slam.c:247-284 per row, in Python: first-insertion list keyed on
-    nearest-point coordinate equality, replaced only by a strictly closer
-    query. Returns the keep mask and the per-row sums of d = ori - near."""
+def _dedup_reference(orc, tree, pos, dist, ori):
+    """src/slam.c:236-284 through the oracle's list builder (orc_rows_dedup,
+    the code orc_slam_localization runs, pinned by the slam8x8 golden):
+    the keep mask and per-row (sum d, centred sum |d - mean|^2, count,
+    queries) over the listed pairs, d = ori - near."""
     R, Cc = pos.shape
-    keep = np.zeros((R, Cc), np.int32)
+    o, nr, _, g = orc.rows_dedup(tree, pos.astype(np.int64), dist, ori)
+    keep = np.zeros(R * Cc, np.int32)
+    keep[g] = 1
     sums = np.zeros((R, 6))
+    rows = g // Cc
+    d = o - nr
     for r in range(R):
-        entries = {}
-        for c in range(Cc):
-            p = int(pos[r, c])
-            if p < 0:
-                continue
-            sums[r, 5] += 1
-            near = tree[r, p]
-            key = tuple(0.0 if v == 0 else float(v) for v in near)
-            if any(v != v for v in key):
-                entries[("nan", c)] = c
-                continue
-            if key in entries:
-                if dist[r, entries[key]] > dist[r, c]:
-                    entries[key] = c
-            else:
-                entries[key] = c
-        for c in entries.values():
-            keep[r, c] = 1
-            d = ori[r, c] - tree[r, int(pos[r, c])]
-            sums[r, :3] += d
-            sums[r, 3] += d @ d
-            sums[r, 4] += 1
-    return keep, sums
+        dr = d[rows == r]
+        sums[r, :3] = dr.sum(axis=0)
+        sums[r, 4] = len(dr)
+        if len(dr):
+            sums[r, 3] = ((dr - dr.mean(axis=0)) ** 2).sum()
+        sums[r, 5] = (pos[r] >= 0).sum()
+    return keep.reshape(R, Cc), sums
 
 
 @pytest.mark.parametrize("integer_mm", [False, True])
-def test_rows_corr_matches_reference_dedup(gpu, integer_mm):
+def test_rows_corr_matches_reference_dedup(gpu, orc, integer_mm):
     """R7 on the GPU (navgpu_rows_corr_dev) against the reference list rule,
     on real per-row trees/queries; integer-mm coordinates make duplicate
     nearest points and distance ties common."""
@@ -508,7 +545,7 @@ def test_rows_corr_matches_reference_dedup(gpu, integer_mm):
     gpu.kd_query_rows_dev(tree, tn, ss, ss, R, Cc, pos, dist)
     gpu.rows_corr_dev(tree, tn, pos, dist, ss, R, Cc, keep, sums)
     gpu.sync()
-    ek, es = _dedup_reference(tree.cpu().numpy(), tn.cpu().numpy(), pos.cpu().numpy(),
+    ek, es = _dedup_reference(orc, tree.cpu().numpy(), pos.cpu().numpy(),
                               dist.cpu().numpy(), src)
     _eq(keep.cpu().numpy(), ek, "kept correspondences")
     np.testing.assert_allclose(sums.cpu().numpy(), es, rtol=1e-12, atol=1e-9)
@@ -547,6 +584,80 @@ def test_shim_l9_stream_fast_adam(monkeypatch, R, Cc, F, steps):
         assert cp == ncp, f"frame {i}: {cp} correspondences vs {ncp}"
         assert abs(attr.error - s.error) <= 1e-9 * max(1.0, s.error)
         last_g, last_o = meas, om
+
+
+def test_shim_l9_long_stream_crosses_map_ring(monkeypatch):
+    """K5 past the reference's 100-frame map (headers/slam.h:12; src/slam.c:395
+    writes globalPointCloud[frameCount] unbounded, the shim keeps a ring):
+    the L9 loop at 54x42 for 120 frames, every pose, error and frame stat
+    bit-exact against the oracle's slam.c restatement, frameCount past 100,
+    and the ring slot of the last frame equal to the oracle's last map."""
+    monkeypatch.setenv("NAVSLAM_QUIET", "1")
+    monkeypatch.delenv("NAVSLAM_ADAM", raising=False)
+    from pyoracle import Oracle, OracleSlam
+    from shimlib import Pos, Shim
+    from navslam.synth import l9_stream, l9_stream_index
+    R, Cc, F, steps = 54, 42, 6, 120
+    frames = l9_stream(R, Cc, F, seed=23)
+    sh = Shim(R, Cc)
+    attr = sh.SLAMAttr()
+    pcs = [sh.cloud(f) for f in frames]
+    zero = np.zeros(6)
+    sh.L.init_slam(C.byref(attr), Pos.of(zero), C.byref(pcs[0]))
+    s = OracleSlam(Oracle(), R, Cc)
+    s.init(zero, frames[0])
+    last_g, last_o = Pos.of(zero), zero
+    for i in range(1, steps + 1):
+        f = l9_stream_index(i, F)
+        meas = sh.L.slam_localization(C.byref(attr), C.byref(pcs[f]), last_g, last_g)
+        sh.L.slam_mapping(C.byref(attr), meas, C.byref(pcs[f]))
+        om, iters, ncp = s.localization(frames[f], last_o, last_o)
+        s.mapping(om, frames[f])
+        _eq(np.array(meas.tolist()), om, f"frame {i} pose")
+        assert attr.error == s.error, f"frame {i} error"
+        q, cp, it = sh.last_frame_stats()
+        assert (cp, it) == (ncp, iters), f"frame {i} stats"
+        last_g, last_o = meas, om
+    assert attr.frameCount == s.frame_count == steps + 1 > 100
+    slot = (attr.frameCount - 1) % 100
+    got = np.frombuffer(bytes(attr.globalPointCloud[slot].pos), np.float64).reshape(R, Cc, 3)
+    _eq(got, s.last_global(), "ring slot of the last frame")
+
+
+@pytest.mark.parametrize("offset", [(0.0, 0.0, 0.0), (1500.0, -700.0, 300.0),
+                                    (2.5e5, 4.0e5, -1.0e5)])
+def test_shim_fast_adam_error_finite_under_offset(monkeypatch, offset):
+    """NAVSLAM_ADAM=fast with the map built at a shifted pose, so the residuals
+    d = ori - near are large against their spread (the case where an
+    uncentred closed form sum |d|^2 - 2 t.S1 + n |t|^2 cancels): the error
+    stays finite and non-negative and matches the oracle's sequential sums.
+    Offset 0 and the same frame: exact correspondences, error 0."""
+    monkeypatch.setenv("NAVSLAM_QUIET", "1")
+    monkeypatch.setenv("NAVSLAM_ADAM", "fast")
+    from pyoracle import Oracle, OracleSlam
+    from shimlib import Pos, Shim
+    from navslam.synth import l9_stream
+    R, Cc = 54, 42
+    frames = l9_stream(R, Cc, 3, seed=29)
+    sh = Shim(R, Cc)
+    s = OracleSlam(Oracle(), R, Cc)
+    mp = np.array(list(offset) + [0.0, 0.0, 0.0])
+    zero = np.zeros(6)
+    for f in range(3):
+        attr = sh.SLAMAttr()
+        pc0 = sh.cloud(frames[0])
+        sh.L.init_slam(C.byref(attr), Pos.of(mp), C.byref(pc0))
+        s.init(mp, frames[0])
+        meas = sh.L.slam_localization(C.byref(attr), C.byref(sh.cloud(frames[f])),
+                                      Pos.of(zero), Pos.of(zero))
+        om, iters, ncp = s.localization(frames[f], zero, zero)
+        q, cp, it = sh.last_frame_stats()
+        assert cp == ncp
+        assert np.isfinite(attr.error) and attr.error >= 0.0
+        assert abs(attr.error - s.error) <= 1e-9 * max(1.0, s.error), (attr.error, s.error)
+        np.testing.assert_allclose(np.array(meas.tolist()), om, rtol=0, atol=1e-6)
+        if f == 0 and offset == (0.0, 0.0, 0.0):
+            assert attr.error == 0.0 == s.error
 
 
 def test_shim_kdtree_api_matches_reference_golden(golden):
