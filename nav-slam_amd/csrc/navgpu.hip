@@ -1149,7 +1149,11 @@ constexpr int kTileMaxW = 64;  // cells per k_knn tile along x, at most
 
 struct __align__(16) Rec16 {  // cell-sorted target: (coords - origin) in f32
   float x, y, z;
-  int idx;
+  int cx;  // x index of its grid cell (the f64 binning's, exact)
+};
+struct __align__(16) TRec {  // cell-sorted target, exact: the reference f64 point + its index
+  double x, y, z;
+  int idx, pad;
 };
 
 constexpr int kBBoxBlocks = 1024;
@@ -1356,7 +1360,7 @@ __global__ __launch_bounds__(kScanBlock) void k_scan_apply(
 //                (bucket, block) and moves to the coarse-bucketed array.
 //  k_bin_fine    one block per bucket: LDS counting sort over the bucket's
 //                2^shift cells, writes start[] for them and every point at its
-//                final cell-sorted position (target: Rec16 + f64 copy;
+//                final cell-sorted position (target: Rec16 + TRec;
 //                query: its index). Order inside a cell is unspecified: the
 //                k-NN result does not depend on it (ties are resolved by
 //                (distance, index) in the exact stage).
@@ -1379,7 +1383,7 @@ struct BinJob {
   BinPt *bin_t;
   int2 *bin_q;    // (idx, cell)
   Rec16 *rec;
-  double *tsort;
+  TRec *tsort;
   int *qperm;
 };
 constexpr int kBinMaxBuckets = 4096;
@@ -1525,14 +1529,18 @@ __device__ void bin_fine_bucket(const BinJob &J, const BinSide &S, const GridPar
       J.qperm[atomicAdd(&cnt[e.y - base], 1)] = e.x;
     } else {
       const int pos = atomicAdd(&cnt[e.cell - base], 1);
-      J.tsort[3 * (size_t)pos] = e.x;
-      J.tsort[3 * (size_t)pos + 1] = e.y;
-      J.tsort[3 * (size_t)pos + 2] = e.z;
+      TRec t;
+      t.x = e.x;
+      t.y = e.y;
+      t.z = e.z;
+      t.idx = e.idx;
+      t.pad = 0;
+      J.tsort[pos] = t;
       Rec16 r;
       r.x = (float)(e.x - G.o[0]);
       r.y = (float)(e.y - G.o[1]);
       r.z = (float)(e.z - G.o[2]);
-      r.idx = e.idx;
+      r.cx = e.cell % G.g[0];
       J.rec[pos] = r;
     }
   };
@@ -1678,11 +1686,15 @@ __device__ __forceinline__ uint32_t knn_key(float d, uint32_t vmask, uint32_t li
 #endif
 }
 
-template <int K, class Runs, class CurF, class IdxF>
+template <int K, int NR, class Runs, class CurF, class GposF>
 __device__ __forceinline__ void knn_one(
-    const GridParams &G, const double *__restrict__ tsort, const double qv[3],
-    const int c[3], size_t q, Runs runs, CurF cursor, IdxF fidx,
+    const GridParams &G, const TRec *__restrict__ tsort, const double qv[3],
+    const int c[3], size_t q, Runs runs, CurF cursor, GposF fgpos,
     int32_t *__restrict__ oidx, double *__restrict__ odist, const KnnLists &L_) {
+  // NR = 9: the block as 9 runs (run | offset ids); NR = 1: one contiguous
+  // range (the column-major tile), the whole key id is the offset
+  constexpr int kOffBits = NR == 1 ? kKeyBits : kRunOffBits;
+  static_assert(NR == 1 || NR == 9, "a 3x3x3 block is 1 or 9 ranges");
   NV_STAMP(ts0);
   const double qr[3] = {qv[0] - G.o[0], qv[1] - G.o[1], qv[2] - G.o[2]};
   const float qf[3] = {(float)qr[0], (float)qr[1], (float)qr[2]};
@@ -1708,16 +1720,16 @@ __device__ __forceinline__ void knn_one(
 #endif
     key[0] = min(key[0], kk);
   };
-  constexpr uint32_t kOffMask = (1u << kRunOffBits) - 1;
+  constexpr uint32_t kOffMask = (1u << kOffBits) - 1;
   const uint32_t vmask = ~kKeyMask;
 #pragma unroll 1
-  for (int r = 0; r < 9; ++r) {
-    int t0, t1, g0;
-    runs(r, t0, t1, g0);
+  for (int r = 0; r < NR; ++r) {
+    int t0, t1;
+    runs(r, t0, t1);
     const int ta = t0 & ~1;
     const int np = (t1 - ta + 1) >> 1;  // pairs the run touches
-    overflow |= (t1 - ta) > (1 << kRunOffBits);
-    const uint32_t rid = (uint32_t)r << kRunOffBits;
+    overflow |= (t1 - ta) > (1 << kOffBits);
+    const uint32_t rid = (uint32_t)r << kOffBits;
     auto cur = cursor(ta);
     if (np > 0) {  // first pair: may start before the run (odd t0) or end past it
       const f2 d = dist2(cur.load());
@@ -1790,32 +1802,37 @@ __device__ __forceinline__ void knn_one(
   if (key[0] != kNoKey) {
 #endif
     int gpos[KL];
+    bool val[KL];
 #pragma unroll
     for (int s = 0; s < KL; ++s) {
-      const bool v = key[s] != kNoKey;
-      const int l = (int)((v ? key[s] : key[0]) & kKeyMask);
+      val[s] = key[s] != kNoKey;
+      const int l = (int)((val[s] ? key[s] : key[0]) & kKeyMask);
 #ifdef NAVGPU_DBG_NODECODE  // timing-only ablation: every slot decodes in run 0
-      const int r = 0, off = l & ((1 << kRunOffBits) - 1);
+      const int r = 0, off = l & (int)kOffMask;
 #else
-      const int r = min(l >> kRunOffBits, 8), off = l & ((1 << kRunOffBits) - 1);
+      const int r = NR == 1 ? 0 : min(l >> kOffBits, NR - 1), off = l & (int)kOffMask;
 #endif
-      int t0, t1, g0;
-      runs(r, t0, t1, g0);
+      int t0, t1;
+      runs(r, t0, t1);
       // record, in the fetch index space; clamped into the run so that a
       // corrupt id can never address outside the staged/sorted arrays
       const int p = min(max((t0 & ~1) + off, t0), max(t1 - 1, t0));
-      ei[s] = v ? fidx(p) : -1;
-      gpos[s] = g0 + (p - t0);
+      gpos[s] = fgpos(p);
     }
 #pragma unroll
     for (int s = 0; s < KL; ++s) {
 #ifdef NAVGPU_DBG_NOF64  // timing-only ablation: f32 key as the distance
       const double dsq = (double)__uint_as_float(key[s] & ~kKeyMask) + gpos[s] * 1e-30;
+      ei[s] = val[s] ? gpos[s] : -1;
 #else
-      const double *tp = tsort + 3 * (size_t)gpos[s];
-      const double px = tp[0], py = tp[1], pz = tp[2];
-      const double ddx = px - qv[0], ddy = py - qv[1], ddz = pz - qv[2];
+      // x, y as one 16-B load, z + idx as one 12-B load (the pad is never read)
+      const TRec *tp = tsort + gpos[s];
+      const double2 xy = *(const double2 *)&tp->x;
+      const double pz = tp->z;
+      const int pid = tp->idx;
+      const double ddx = xy.x - qv[0], ddy = xy.y - qv[1], ddz = pz - qv[2];
       const double dsq = ddx * ddx + ddy * ddy + ddz * ddz;  // utils/kdtree.c:16
+      ei[s] = val[s] ? pid : -1;
 #endif
       ed[s] = ei[s] >= 0 ? __builtin_sqrt(dsq) : INFINITY;
       // an inf/NaN distance is never a neighbour (kdtree.c:117)
@@ -1825,6 +1842,7 @@ __device__ __forceinline__ void knn_one(
         ok = false;
       }
     }
+
   } else {
 #pragma unroll
     for (int s = 0; s < KL; ++s) {
@@ -1931,6 +1949,9 @@ __device__ __forceinline__ void knn_one(
 #endif
 constexpr int kTileThreads = NAVGPU_TILE_THREADS;
 constexpr int kTileRec = NAVGPU_TILE_REC;  // records staged per tile (16 B each)
+#ifndef NAVGPU_STAGE_U
+#define NAVGPU_STAGE_U 4  // records per thread per staging batch (8: 140 VGPRs, one block fewer per CU)
+#endif
 
 // Global-mode exact k-NN over tiles of W consecutive cells of one grid row.
 // A tile stages the 9 neighbouring row segments (cells xa-1 .. xb+1) of the
@@ -1939,9 +1960,15 @@ constexpr int kTileRec = NAVGPU_TILE_REC;  // records staged per tile (16 B each
 // 8 XCDs in contiguous ranges (block b runs on XCD b % 8 under the observed
 // round-robin placement; a different placement only costs L2 hits), so each
 // XCD's L2 holds only its slab of the cloud.
+// The LDS tile is COLUMN-major: for each x cell j of the segment, the records
+// of its 9 (y, z) rows follow one another. A query's 3x3x3 block (columns
+// x-1 .. x+1, all 9 rows) is then one contiguous record range, walked as one
+// loop: a wave's trip count is the longest block among its lanes (neighbouring
+// blocks share 18 of 27 cells), not the sum over 9 runs of each run's longest,
+// and there is one run setup and one masked pair per query instead of 9.
 // GLOBAL = false: the tile pass; a tile whose segments exceed the LDS budget
 // is appended to the overflow list. GLOBAL = true: the overflow tiles, read
-// straight from the global record array.
+// straight from the global record array as 9 runs.
 template <int K, bool GLOBAL>
 #ifndef NAVGPU_KNN_MINW
 #define NAVGPU_KNN_MINW 1
@@ -1953,15 +1980,20 @@ template <int K, bool GLOBAL>
 #endif
 __global__ __launch_bounds__(kTileThreads, NAVGPU_KNN_MINW) NAVGPU_KNN_ATTR void k_knn(
     const GridParams *__restrict__ gp, const int *__restrict__ start,
-    const Rec16 *__restrict__ rec, const double *__restrict__ tsort,
+    const Rec16 *__restrict__ rec, const TRec *__restrict__ tsort,
     const double *__restrict__ qs, const int *__restrict__ qstart,
     const int *__restrict__ qperm, int32_t *__restrict__ oidx,
     double *__restrict__ odist, KnnLists L_) {
-  // pair-interleaved records: pair P = records 2P, 2P+1 as x0 x1 y0 y1 z0 z1
-  // i0 i1 (32 B), so one b128 + one b64 read gives packed operands; two
-  // spare pairs absorb the read-ahead past a run's end
+  // pair-interleaved records: pair P = LDS slots 2P, 2P+1 as x0 x1 y0 y1 z0 z1
+  // g0 g1 (32 B; g = the record's cell-sorted position), so one b128 + one
+  // b64 read gives packed operands; two spare pairs absorb the read-ahead
+  // past a range's end
   __shared__ __attribute__((aligned(16))) float spair[GLOBAL ? 8 : (kTileRec / 2 + 2) * 8];
   __shared__ int soff[9][kTileMaxW + 4];
+  // LDS slot of the record at cell-sorted position g of cell (row r, column
+  // j) = cbase[r][j] + g; colst[j] = first slot of column j (j = 0: cell xa-1)
+  __shared__ int cbase[GLOBAL ? 1 : 9][kTileMaxW + 4];
+  __shared__ int colst[GLOBAL ? 1 : kTileMaxW + 4];
   __shared__ int sbase[10];
   const GridParams G = *gp;
   const int W = G.tile_w;
@@ -2018,16 +2050,47 @@ __global__ __launch_bounds__(kTileThreads, NAVGPU_KNN_MINW) NAVGPU_KNN_ATTR void
     }
     __syncthreads();
     if (!GLOBAL) {
-      if (threadIdx.x < kWave) {  // row segment bases: a 9-lane prefix sum
-        const int r = threadIdx.x;
-        int len = r < 9 ? soff[r][ncell - 1] - soff[r][0] : 0;
-        int inc = len;
+      if (threadIdx.x < kWave) {
+        const int lane = threadIdx.x;
+        {  // row segment bases (the coalesced copy's source order): a 9-lane prefix sum
+          int len = lane < 9 ? soff[lane][ncell - 1] - soff[lane][0] : 0;
+          int inc = len;
 #pragma unroll
-        for (int o = 1; o < 16; o <<= 1) {
-          const int t = __shfl_up(inc, o, kWave);
-          if (r >= o) inc += t;
+          for (int o = 1; o < 16; o <<= 1) {
+            const int t = __shfl_up(inc, o, kWave);
+            if (lane >= o) inc += t;
+          }
+          if (lane <= 9) sbase[lane] = inc - len;  // lane 9: the total
         }
-        if (r <= 9) sbase[r] = inc - len;  // r = 9: the total
+        // the column-major layout: lane l owns columns 2l and 2l + 1 of the
+        // W + 2 (<= kTileMaxW + 2 <= 128)
+        const int ncol = ncell - 1;
+        const int j0 = 2 * lane, j1 = j0 + 1;
+        int n0[9], n1[9], s0 = 0, s1 = 0;
+#pragma unroll
+        for (int r = 0; r < 9; ++r) {
+          n0[r] = j0 < ncol ? soff[r][j0 + 1] - soff[r][j0] : 0;
+          n1[r] = j1 < ncol ? soff[r][j1 + 1] - soff[r][j1] : 0;
+          s0 += n0[r];
+          s1 += n1[r];
+        }
+        int inc = s0 + s1;
+#pragma unroll
+        for (int o = 1; o < kWave; o <<= 1) {
+          const int t = __shfl_up(inc, o, kWave);
+          if (lane >= o) inc += t;
+        }
+        const int ex = inc - (s0 + s1);
+        if (j0 <= ncol) colst[j0] = ex;  // colst[ncol] = the total
+        if (j1 <= ncol) colst[j1] = ex + s0;
+        int a0 = ex, a1 = ex + s0;
+#pragma unroll
+        for (int r = 0; r < 9; ++r) {
+          if (j0 < ncol) cbase[r][j0] = a0 - soff[r][j0];
+          if (j1 < ncol) cbase[r][j1] = a1 - soff[r][j1];
+          a0 += n0[r];
+          a1 += n1[r];
+        }
       }
       __syncthreads();
       const int total = sbase[9];
@@ -2041,19 +2104,26 @@ __global__ __launch_bounds__(kTileThreads, NAVGPU_KNN_MINW) NAVGPU_KNN_ATTR void
       for (int u = 0; u < 10; ++u) sb[u] = sbase[u];
 #pragma unroll
       for (int u = 0; u < 9; ++u) s0[u] = soff[u][0] - sb[u];  // global = e + s0[r]
-      constexpr int U = 8;  // records per thread per batch
+      const int jmax = ncell - 2;
+      constexpr int U = NAVGPU_STAGE_U;  // records per thread per batch
       for (int e0 = 0; e0 < total; e0 += U * (int)blockDim.x) {
         Rec16 v[U];
+        int gg[U], rr[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
           const int e = e0 + u * (int)blockDim.x + (int)threadIdx.x;
-          if (e < total) {
-            int g = e + s0[0];
+          int g = e + s0[0], r = 0;
 #pragma unroll
-            for (int w = 1; w < 9; ++w) g = e >= sb[w] ? e + s0[w] : g;
+          for (int w = 1; w < 9; ++w) {
+            g = e >= sb[w] ? e + s0[w] : g;
+            r = e >= sb[w] ? w : r;
+          }
+          gg[u] = g;
+          rr[u] = r;
+          if (e < total) {
 #ifdef NAVGPU_DBG_NOSTAGE  // timing-only ablation: no record loads
             v[u].x = v[u].y = v[u].z = (float)g;
-            v[u].idx = g;
+            v[u].cx = xa;
 #else
             v[u] = rec[g];
 #endif
@@ -2063,11 +2133,15 @@ __global__ __launch_bounds__(kTileThreads, NAVGPU_KNN_MINW) NAVGPU_KNN_ATTR void
         for (int u = 0; u < U; ++u) {
           const int e = e0 + u * (int)blockDim.x + (int)threadIdx.x;
           if (e < total) {
-            float *d = spair + (e >> 1) * 8 + (e & 1);
+            // the record's column (its cell lies in xa-1 .. xb+1; clamped so
+            // that a corrupt value cannot address outside the tile)
+            const int j = min(max(v[u].cx - xa + 1, 0), jmax);
+            const int slot = cbase[rr[u]][j] + gg[u];
+            float *d = spair + (slot >> 1) * 8 + (slot & 1);
             d[0] = v[u].x;
             d[2] = v[u].y;
             d[4] = v[u].z;
-            d[6] = __int_as_float(v[u].idx);
+            d[6] = __int_as_float(gg[u]);
           }
         }
       }
@@ -2085,26 +2159,24 @@ __global__ __launch_bounds__(kTileThreads, NAVGPU_KNN_MINW) NAVGPU_KNN_ATTR void
       const size_t q = (size_t)qperm[qi];
       const double qv[3] = {qs[3 * q], qs[3 * q + 1], qs[3 * q + 2]};
       const int c[3] = {cell_axis(qv[0], G, 0), y, z};
-      const int i = c[0] - xa;
+      const int i = c[0] - xa;  // columns i .. i+2 = cells c-1 .. c+1
       if (!GLOBAL) {
-        knn_one<K>(G, tsort, qv, c, q,
-                   [&](int r, int &t0, int &t1, int &g0) {
-                     const int sh = sbase[r] - soff[r][0];
-                     g0 = soff[r][i];
-                     t0 = g0 + sh;
-                     t1 = soff[r][i + 3] + sh;
-                   },
-                   [&](int t) { return LdsPairCursor{spair + (t >> 1) * 8}; },
-                   [&](int p) { return __float_as_int(spair[(p >> 1) * 8 + 6 + (p & 1)]); },
-                   oidx, odist, L_);
+        knn_one<K, 1>(G, tsort, qv, c, q,
+                      [&](int, int &t0, int &t1) {
+                        t0 = colst[i];
+                        t1 = colst[i + 3];
+                      },
+                      [&](int t) { return LdsPairCursor{spair + (t >> 1) * 8}; },
+                      [&](int p) { return __float_as_int(spair[(p >> 1) * 8 + 6 + (p & 1)]); },
+                      oidx, odist, L_);
       } else {
-        knn_one<K>(G, tsort, qv, c, q,
-                   [&](int r, int &t0, int &t1, int &g0) {
-                     t0 = g0 = soff[r][i];
-                     t1 = soff[r][i + 3];
-                   },
-                   [&](int t) { return RecPairCursor{rec + t}; },
-                   [&](int p) { return rec[p].idx; }, oidx, odist, L_);
+        knn_one<K, 9>(G, tsort, qv, c, q,
+                      [&](int r, int &t0, int &t1) {
+                        t0 = soff[r][i];
+                        t1 = soff[r][i + 3];
+                      },
+                      [&](int t) { return RecPairCursor{rec + t}; },
+                      [&](int p) { return p; }, oidx, odist, L_);
       }
     }
     NV_STAMP(tb2);
@@ -2172,17 +2244,17 @@ __device__ __forceinline__ void knn_wave_merge(double *kd, int *ki, double *md, 
 // into the lane's sorted list when within thr
 template <int K>
 __device__ __forceinline__ void knn_visit(const Rec16 &rr, size_t t,
-                                          const double *__restrict__ tsort,
+                                          const TRec *__restrict__ tsort,
                                           const double qv[3], const float qf[3],
                                           double thr, float thr_f, double *kd, int *ki) {
   const float fx = rr.x - qf[0], fy = rr.y - qf[1], fz = rr.z - qf[2];
   const float d2f = __builtin_fmaf(fz, fz, __builtin_fmaf(fy, fy, fx * fx));
   if (!(d2f <= thr_f)) return;
-  const double *tp = tsort + 3 * t;
-  const double ddx = tp[0] - qv[0], ddy = tp[1] - qv[1], ddz = tp[2] - qv[2];
+  const TRec tp = tsort[t];
+  const double ddx = tp.x - qv[0], ddy = tp.y - qv[1], ddz = tp.z - qv[2];
   const double dsq = ddx * ddx + ddy * ddy + ddz * ddz;  // utils/kdtree.c:16
   if (!(dsq <= thr)) return;
-  knn_insert<K>(kd, ki, __builtin_sqrt(dsq), rr.idx);
+  knn_insert<K>(kd, ki, __builtin_sqrt(dsq), tp.idx);
 }
 
 constexpr int kSlowMaxR = 3;  // one-shot cube: at most (2R+1)^2 = 49 rows
@@ -2199,7 +2271,7 @@ constexpr int kSlowMaxR = 3;  // one-shot cube: at most (2R+1)^2 = 49 rows
 template <int K>
 __global__ __launch_bounds__(256) void k_knn_slow(
     const GridParams *__restrict__ gp, const int *__restrict__ start,
-    const Rec16 *__restrict__ rec, const double *__restrict__ tsort,
+    const Rec16 *__restrict__ rec, const TRec *__restrict__ tsort,
     const double *__restrict__ qs, int32_t *__restrict__ oidx,
     double *__restrict__ odist, KnnLists L_) {
   __shared__ double sd[4][kWave];  // per-wave survivor buffers (256 threads)
@@ -3048,7 +3120,7 @@ static int knn_run(navgpu_ctx *ctx, const double *tgt, size_t nt, const double *
   GridParams *gp;
   int *tab, *offs, *tstart, *qstart, *bsum, *qperm;
   Rec16 *rec = nullptr;
-  double *tsort = nullptr;
+  TRec *tsort = nullptr;
   BinPt *bin_t = nullptr;
   int2 *bin_q;
   RC(ws(ctx, kBBox, (size_t)kBBoxBlocks * 6, &part));
@@ -3063,7 +3135,7 @@ static int knn_run(navgpu_ctx *ctx, const double *tgt, size_t nt, const double *
   if (nt) {
     RC(ws(ctx, kSlotBuf, nt, &bin_t));
     RC(ws(ctx, kRec, nt + 2, &rec));  // + 2: a last pair may read one past the end
-    RC(ws(ctx, kTSort, 3 * nt, &tsort));
+    RC(ws(ctx, kTSort, nt, &tsort));
   }
   RC(ws(ctx, kQCell, nq, &bin_q));
   RC(ws(ctx, kQPerm, nq, &qperm));
