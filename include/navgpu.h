@@ -199,6 +199,9 @@ int navgpu_timing_count(navgpu_ctx *ctx, const char *name);
  * for the exact ring search (synchronises). Recorded only when the context
  * was created with NAVGPU_KNN_STATS=1 in the environment; -1 otherwise. */
 long long navgpu_knn_fallbacks(navgpu_ctx *ctx);
+/* Diagnostic: k_knn tiles of the last navgpu_knn_* call whose neighbourhood
+ * exceeded the LDS tile budget and ran from global memory (synchronises). */
+long long navgpu_knn_overflows(navgpu_ctx *ctx);
 
 #ifdef __cplusplus
 }

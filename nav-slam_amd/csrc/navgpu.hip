@@ -1131,15 +1131,23 @@ __global__ __launch_bounds__(kCorrBlock) void k_rows_corr(
 // array: a query's 3x3x3 neighbourhood is 9 contiguous "runs".
 struct GridParams {
   double o[3];      // origin = target bbox min
-  double h, inv_h;  // cell edge
+  double e[3], inv_e[3];  // cell edge per axis: x h / sx, y and z h
+  double h;         // the coarse edge
   double delta;     // slack on cell boxes (cell assignment is f64 arithmetic)
   double emax;      // largest bbox extent
   int g[3];
   int ncells;
+  int sx;           // x cells per h: a query's block is cells x-sx .. x+sx,
+                    // y-1 .. y+1, z-1 .. z+1 (the reach is >= h on every axis)
   int tile_w;       // cells per k_knn tile along x
 };
 
-constexpr int kTileMaxW = 64;  // cells per k_knn tile along x, at most
+// soff entries per staged row of a k_knn tile (W + 2 sx + 1 <= kTileCols)
+constexpr int kTileCols = 136;
+constexpr int kMaxSx = 8;
+#ifndef NAVGPU_KNN_SX
+#define NAVGPU_KNN_SX 1  // sx = 2: query stage 183 -> 177 us, build 99 -> 109 us (K3)
+#endif
 #ifndef NAVGPU_TILE_QUERIES
 #define NAVGPU_TILE_QUERIES 165.0  // target queries per k_knn tile
 #endif
@@ -1208,7 +1216,7 @@ __global__ __launch_bounds__(256) void k_bbox_partial(const double *__restrict__
 // at `cap` cells.
 __global__ __launch_bounds__(256) void k_grid_params(const double *__restrict__ part,
                                                      int nparts, size_t n, int cap,
-                                                     double occ, size_t nq,
+                                                     double occ, int sx, size_t nq,
                                                      GridParams *gp, int *counters) {
   // also resets the call's k-NN counters (overflow tiles, slow queries): one
   // launch fewer than a memset
@@ -1243,8 +1251,10 @@ __global__ __launch_bounds__(256) void k_grid_params(const double *__restrict__ 
     for (int a = 0; a < 3; ++a) {
       G.o[a] = 0.0;
       G.g[a] = 1;
+      G.e[a] = G.inv_e[a] = 1.0;
     }
-    G.h = G.inv_h = G.delta = 1.0;
+    G.h = G.delta = 1.0;
+    G.sx = 1;
     G.emax = 0.0;
     G.ncells = 1;
     G.tile_w = 1;
@@ -1261,7 +1271,8 @@ __global__ __launch_bounds__(256) void k_grid_params(const double *__restrict__ 
   for (int it = 0; it < 200; ++it) {
     long long tot = 1;
     for (int a = 0; a < 3; ++a) {
-      double ga = floor(ext[a] / h) + 1.0;  // covers [lo, lo + ext] inclusive
+      const double ea = a == 0 ? h / sx : h;
+      double ga = floor(ext[a] / ea) + 1.0;  // covers [lo, lo + ext] inclusive
       if (ga > 2048) ga = 2048;
       g[a] = (int)ga;
       tot *= g[a];
@@ -1271,29 +1282,33 @@ __global__ __launch_bounds__(256) void k_grid_params(const double *__restrict__ 
   }
   for (int a = 0; a < 3; ++a) G.o[a] = lo[a];
   G.h = h;
-  G.inv_h = 1.0 / h;
+  G.sx = sx;
+  for (int a = 0; a < 3; ++a) {
+    G.e[a] = a == 0 ? h / sx : h;
+    G.inv_e[a] = 1.0 / G.e[a];
+  }
   G.delta = 1e-7 * (emax + h);
   G.emax = emax;
   G.g[0] = g[0];
   G.g[1] = g[1];
   G.g[2] = g[2];
   G.ncells = g[0] * g[1] * g[2];
-  // tile width: ~220 queries per 256-thread tile, and its 9 staged row
-  // segments of W+2 cells within ~90 % of the LDS record budget
+  // tile width: ~165 queries per 192-thread tile, and its 9 staged row
+  // segments of W + 2 sx cells within ~90 % of the LDS record budget
   const double occ_q = (double)nq / G.ncells, occ_t = (double)n / G.ncells;
   double w = fmin(NAVGPU_TILE_QUERIES / fmax(occ_q, 1e-9),
-                  0.9 * NAVGPU_TILE_REC / (9.0 * fmax(occ_t, 1e-9)) - 2.0);
+                  0.9 * NAVGPU_TILE_REC / (9.0 * fmax(occ_t, 1e-9)) - 2.0 * sx);
   // balanced: the fewest tiles per grid row at that width, then equal widths
   // (a ragged last tile would pay a full staging + barrier cycle for a few
   // cells)
-  const int wmax = (int)fmax(1.0, fmin((double)kTileMaxW, floor(w)));
+  const int wmax = (int)fmax(1.0, fmin((double)(kTileCols - 1 - 2 * sx), floor(w)));
   const int tpr = (G.g[0] + wmax - 1) / wmax;
   G.tile_w = (G.g[0] + tpr - 1) / tpr;
   *gp = G;
 }
 
 __device__ __forceinline__ int cell_axis(double v, const GridParams &G, int a) {
-  const double t = (v - G.o[a]) * G.inv_h;
+  const double t = (v - G.o[a]) * G.inv_e[a];
   if (!(t >= 0.0)) return 0;  // below the grid, or NaN
   if (t >= (double)G.g[a]) return G.g[a] - 1;
   return (int)t;
@@ -1583,14 +1598,30 @@ __device__ __forceinline__ double box_d2(const GridParams &G, const double *qv,
   double s = 0.0;
 #pragma unroll
   for (int a = 0; a < 3; ++a) {
-    const double bl = G.o[a] + lo[a] * G.h - G.delta;
-    const double bh = G.o[a] + (hi[a] + 1) * G.h + G.delta;
+    const double bl = G.o[a] + lo[a] * G.e[a] - G.delta;
+    const double bh = G.o[a] + (hi[a] + 1) * G.e[a] + G.delta;
     // boundary cells also hold everything clamped into them
     const double e = fmax(0.0, fmax(lo[a] > 0 ? bl - qv[a] : 0.0,
                                      hi[a] < G.g[a] - 1 ? qv[a] - bh : 0.0));
     s += e * e;
   }
   return s;
+}
+
+// Distance from q (in cell c) to the outside of its block of radius r: cells
+// x - r sx .. x + r sx, y - r .. y + r, z - r .. z + r. A block face on the
+// grid boundary does not count (the boundary cells hold everything clamped
+// into them); INFINITY when every face is.
+__device__ __forceinline__ double block_reach(const GridParams &G, const double *qv,
+                                              const int c[3], int r) {
+  double L = INFINITY;
+#pragma unroll
+  for (int a = 0; a < 3; ++a) {
+    const int ra = a == 0 ? r * G.sx : r;
+    if (c[a] - ra > 0) L = fmin(L, qv[a] - (G.o[a] + (c[a] - ra) * G.e[a]));
+    if (c[a] + ra < G.g[a] - 1) L = fmin(L, (G.o[a] + (c[a] + ra + 1) * G.e[a]) - qv[a]);
+  }
+  return L;
 }
 
 // f32 admission bound for an f64 dsq bound T: every candidate whose exact
@@ -1773,13 +1804,8 @@ __device__ __forceinline__ void knn_one(
   }
   NV_STAMP(ts1);
   NV_STAMP_ADD(3, ts0, ts1);
-  // anything outside the 3x3x3 block is at least L away
-  double L = INFINITY;
-#pragma unroll
-  for (int a = 0; a < 3; ++a) {
-    if (c[a] - 1 > 0) L = fmin(L, qv[a] - (G.o[a] + (c[a] - 1) * G.h));
-    if (c[a] + 1 < G.g[a] - 1) L = fmin(L, (G.o[a] + (c[a] + 2) * G.h) - qv[a]);
-  }
+  // anything outside the block (x +- sx, y +- 1, z +- 1 cells) is at least L away
+  const double L = block_reach(G, qv, c, 1);
   double B = INFINITY;  // lower bound on the exact dsq of every excluded point
   if (L < INFINITY) {
     const double Lg = L - 2.0 * G.delta;
@@ -1896,7 +1922,8 @@ __device__ __forceinline__ void knn_one(
     ok = ok && B == INFINITY;  // fewer than K neighbours: only if all was seen
 #if defined(NAVGPU_DBG_NOINSERT) || defined(NAVGPU_DBG_NOEXACT) || \
     defined(NAVGPU_DBG_NOF64) || defined(NAVGPU_DBG_NOSTAGE) || \
-    defined(NAVGPU_DBG_NODECODE) || defined(NAVGPU_DBG_NOSORT)
+    defined(NAVGPU_DBG_NODECODE) || defined(NAVGPU_DBG_NOSORT) || \
+    defined(NAVGPU_DBG_STAGE_ONCE)
   ok = true;  // timing-only ablation builds: never take the slow path
 #endif
   if (ok) {
@@ -1950,7 +1977,7 @@ __device__ __forceinline__ void knn_one(
 constexpr int kTileThreads = NAVGPU_TILE_THREADS;
 constexpr int kTileRec = NAVGPU_TILE_REC;  // records staged per tile (16 B each)
 #ifndef NAVGPU_STAGE_U
-#define NAVGPU_STAGE_U 4  // records per thread per staging batch (8: 140 VGPRs, one block fewer per CU)
+#define NAVGPU_STAGE_U 2  // records per thread per staging batch (4: 188.8 us, 8: 140 VGPRs, one block fewer per CU)
 #endif
 
 // Global-mode exact k-NN over tiles of W consecutive cells of one grid row.
@@ -1989,27 +2016,25 @@ __global__ __launch_bounds__(kTileThreads, NAVGPU_KNN_MINW) NAVGPU_KNN_ATTR void
   // b64 read gives packed operands; two spare pairs absorb the read-ahead
   // past a range's end
   __shared__ __attribute__((aligned(16))) float spair[GLOBAL ? 8 : (kTileRec / 2 + 2) * 8];
-  __shared__ int soff[9][kTileMaxW + 4];
-  // LDS slot of the record at cell-sorted position g of cell (row r, column
-  // j) = cbase[r][j] + g; colst[j] = first slot of column j (j = 0: cell xa-1)
-  __shared__ int cbase[GLOBAL ? 1 : 9][kTileMaxW + 4];
-  __shared__ int colst[GLOBAL ? 1 : kTileMaxW + 4];
-  __shared__ int sbase[10];
+  // soff[r][i] = first record of cell xa - sx + i of row r; then, in place
+  // (tile pass), cbase[r][j]: the LDS slot of the record at cell-sorted
+  // position g of cell (row r, column j) is cbase[r][j] + g
+  __shared__ int soff[9][kTileCols];
+  __shared__ int colst[GLOBAL ? 1 : kTileCols];  // first slot of column j (j = 0: cell xa - sx)
+  __shared__ int scratch[kTileThreads / kWave + 1];
   const GridParams G = *gp;
-  const int W = G.tile_w;
+  const int W = G.tile_w, sx = G.sx;
   const int tpr = (G.g[0] + W - 1) / W;
-  long long t_lo, t_hi, step, first;
+  long long t_hi, step, first;
   if (GLOBAL) {
-    t_lo = 0;
     t_hi = *L_.n_ovf;
     first = blockIdx.x;
     step = gridDim.x;
   } else {
     const long long ntiles = (long long)tpr * G.g[1] * G.g[2];
     const int xcd = blockIdx.x & 7;
-    t_lo = ntiles * xcd / 8;
     t_hi = ntiles * (xcd + 1) / 8;
-    first = t_lo + (blockIdx.x >> 3);
+    first = ntiles * xcd / 8 + (blockIdx.x >> 3);
     step = gridDim.x >> 3;
   }
   for (long long it = first; it < t_hi; it += step) {
@@ -2018,7 +2043,10 @@ __global__ __launch_bounds__(kTileThreads, NAVGPU_KNN_MINW) NAVGPU_KNN_ATTR void
     const int row = (int)(tile / tpr), chunk = (int)(tile % tpr);
     const int y = row % G.g[1], z = row / G.g[1];
     const int xa = chunk * W, xb = min(xa + W, G.g[0]) - 1;
-    const int ncell = xb - xa + 4;  // soff[r][i] = first record of cell xa-1+i
+    const int ncell = xb - xa + 2 + 2 * sx;  // soff entries per row: cells xa-sx .. xb+sx+1
+#ifdef NAVGPU_DBG_STAGE_ONCE  // timing-only ablation: the first tile's staging serves all
+    if (it == first) {
+#endif
     // staging is latency-bound: every thread issues all its global loads
     // before it writes any of them to LDS
     {
@@ -2036,7 +2064,7 @@ __global__ __launch_bounds__(kTileThreads, NAVGPU_KNN_MINW) NAVGPU_KNN_ATTR void
             run_dydz(r, dy, dz);
             const int yy = y + dy, zz = z + dz;
             if (yy >= 0 && yy < G.g[1] && zz >= 0 && zz < G.g[2]) {
-              const int x = min(max(xa - 1 + i, 0), G.g[0]);  // x = gx: row end
+              const int x = min(max(xa - sx + i, 0), G.g[0]);  // x = gx: row end
               v[u] = start[(zz * G.g[1] + yy) * G.g[0] + x];
             }
           }
@@ -2044,67 +2072,48 @@ __global__ __launch_bounds__(kTileThreads, NAVGPU_KNN_MINW) NAVGPU_KNN_ATTR void
 #pragma unroll
         for (int u = 0; u < U; ++u) {
           const int e = e0 + u * (int)blockDim.x + (int)threadIdx.x;
-          if (e < nsoff) (&soff[0][0])[(e / ncell) * (kTileMaxW + 4) + e % ncell] = v[u];
+          if (e < nsoff) (&soff[0][0])[(e / ncell) * kTileCols + e % ncell] = v[u];
         }
       }
     }
     __syncthreads();
+    int sb[10], s0[9];  // row segment bases (staging index) and global offsets
     if (!GLOBAL) {
-      if (threadIdx.x < kWave) {
-        const int lane = threadIdx.x;
-        {  // row segment bases (the coalesced copy's source order): a 9-lane prefix sum
-          int len = lane < 9 ? soff[lane][ncell - 1] - soff[lane][0] : 0;
-          int inc = len;
+      // the copy's source order: the 9 row segments one after another
+      sb[0] = 0;
 #pragma unroll
-          for (int o = 1; o < 16; o <<= 1) {
-            const int t = __shfl_up(inc, o, kWave);
-            if (lane >= o) inc += t;
-          }
-          if (lane <= 9) sbase[lane] = inc - len;  // lane 9: the total
-        }
-        // the column-major layout: lane l owns columns 2l and 2l + 1 of the
-        // W + 2 (<= kTileMaxW + 2 <= 128)
-        const int ncol = ncell - 1;
-        const int j0 = 2 * lane, j1 = j0 + 1;
-        int n0[9], n1[9], s0 = 0, s1 = 0;
-#pragma unroll
-        for (int r = 0; r < 9; ++r) {
-          n0[r] = j0 < ncol ? soff[r][j0 + 1] - soff[r][j0] : 0;
-          n1[r] = j1 < ncol ? soff[r][j1 + 1] - soff[r][j1] : 0;
-          s0 += n0[r];
-          s1 += n1[r];
-        }
-        int inc = s0 + s1;
-#pragma unroll
-        for (int o = 1; o < kWave; o <<= 1) {
-          const int t = __shfl_up(inc, o, kWave);
-          if (lane >= o) inc += t;
-        }
-        const int ex = inc - (s0 + s1);
-        if (j0 <= ncol) colst[j0] = ex;  // colst[ncol] = the total
-        if (j1 <= ncol) colst[j1] = ex + s0;
-        int a0 = ex, a1 = ex + s0;
-#pragma unroll
-        for (int r = 0; r < 9; ++r) {
-          if (j0 < ncol) cbase[r][j0] = a0 - soff[r][j0];
-          if (j1 < ncol) cbase[r][j1] = a1 - soff[r][j1];
-          a0 += n0[r];
-          a1 += n1[r];
-        }
+      for (int u = 0; u < 9; ++u) {
+        const int lo = soff[u][0];
+        sb[u + 1] = sb[u] + (soff[u][ncell - 1] - lo);
+        s0[u] = lo - sb[u];  // global = e + s0[r]
       }
-      __syncthreads();
-      const int total = sbase[9];
+      // the column-major layout: thread j owns column j of the W + 2 sx
+      const int ncol = ncell - 1, j = (int)threadIdx.x;
+      int n[9], sv[9], cs = 0;
+#pragma unroll
+      for (int r = 0; r < 9; ++r) {
+        sv[r] = j < ncol ? soff[r][j] : 0;
+        n[r] = j < ncol ? soff[r][j + 1] - sv[r] : 0;
+        cs += n[r];
+      }
+      int total;
+      const int cex = block_excl_scan(cs, scratch, &total);  // barriers: soff reads done
       if (total > kTileRec) {  // uniform: defer the tile to the global pass
         if (threadIdx.x == 0) L_.ovf_tiles[atomicAdd(L_.n_ovf, 1)] = (int)tile;
         __syncthreads();
         continue;
       }
-      int sb[10], s0[9];
+      if (j <= ncol) colst[j] = cex;  // colst[ncol] = the total
+      if (j < ncol) {
+        int a = cex;
 #pragma unroll
-      for (int u = 0; u < 10; ++u) sb[u] = sbase[u];
-#pragma unroll
-      for (int u = 0; u < 9; ++u) s0[u] = soff[u][0] - sb[u];  // global = e + s0[r]
-      const int jmax = ncell - 2;
+        for (int r = 0; r < 9; ++r) {
+          soff[r][j] = a - sv[r];  // cbase
+          a += n[r];
+        }
+      }
+      __syncthreads();
+      const int jmax = ncol - 1;
       constexpr int U = NAVGPU_STAGE_U;  // records per thread per batch
       for (int e0 = 0; e0 < total; e0 += U * (int)blockDim.x) {
         Rec16 v[U];
@@ -2133,10 +2142,10 @@ __global__ __launch_bounds__(kTileThreads, NAVGPU_KNN_MINW) NAVGPU_KNN_ATTR void
         for (int u = 0; u < U; ++u) {
           const int e = e0 + u * (int)blockDim.x + (int)threadIdx.x;
           if (e < total) {
-            // the record's column (its cell lies in xa-1 .. xb+1; clamped so
-            // that a corrupt value cannot address outside the tile)
-            const int j = min(max(v[u].cx - xa + 1, 0), jmax);
-            const int slot = cbase[rr[u]][j] + gg[u];
+            // the record's column (its cell lies in xa-sx .. xb+sx; clamped
+            // so that a corrupt value cannot address outside the tile)
+            const int jj = min(max(v[u].cx - xa + sx, 0), jmax);
+            const int slot = soff[rr[u]][jj] + gg[u];
             float *d = spair + (slot >> 1) * 8 + (slot & 1);
             d[0] = v[u].x;
             d[2] = v[u].y;
@@ -2147,6 +2156,9 @@ __global__ __launch_bounds__(kTileThreads, NAVGPU_KNN_MINW) NAVGPU_KNN_ATTR void
       }
       __syncthreads();
     }
+#ifdef NAVGPU_DBG_STAGE_ONCE
+    }
+#endif
     NV_STAMP(tb1);
     NV_STAMP_ADD(1, tb0, tb1);
     NV_STAMP_ADD(6, 0ull, 1ull);
@@ -2159,12 +2171,12 @@ __global__ __launch_bounds__(kTileThreads, NAVGPU_KNN_MINW) NAVGPU_KNN_ATTR void
       const size_t q = (size_t)qperm[qi];
       const double qv[3] = {qs[3 * q], qs[3 * q + 1], qs[3 * q + 2]};
       const int c[3] = {cell_axis(qv[0], G, 0), y, z};
-      const int i = c[0] - xa;  // columns i .. i+2 = cells c-1 .. c+1
+      const int i = c[0] - xa;  // columns i .. i + 2 sx = cells c - sx .. c + sx
       if (!GLOBAL) {
         knn_one<K, 1>(G, tsort, qv, c, q,
                       [&](int, int &t0, int &t1) {
                         t0 = colst[i];
-                        t1 = colst[i + 3];
+                        t1 = colst[i + 2 * sx + 1];
                       },
                       [&](int t) { return LdsPairCursor{spair + (t >> 1) * 8}; },
                       [&](int p) { return __float_as_int(spair[(p >> 1) * 8 + 6 + (p & 1)]); },
@@ -2173,7 +2185,7 @@ __global__ __launch_bounds__(kTileThreads, NAVGPU_KNN_MINW) NAVGPU_KNN_ATTR void
         knn_one<K, 9>(G, tsort, qv, c, q,
                       [&](int r, int &t0, int &t1) {
                         t0 = soff[r][i];
-                        t1 = soff[r][i + 3];
+                        t1 = soff[r][i + 2 * sx + 1];
                       },
                       [&](int t) { return RecPairCursor{rec + t}; },
                       [&](int p) { return p; }, oidx, odist, L_);
@@ -2281,7 +2293,7 @@ __global__ __launch_bounds__(256) void k_knn_slow(
   const int lane = threadIdx.x & (kWave - 1);
   const int wave = (int)((blockIdx.x * blockDim.x + threadIdx.x) / kWave);
   const int nwaves = (int)(gridDim.x * blockDim.x / kWave);
-  const int gmax = max(G.g[0], max(G.g[1], G.g[2]));
+  const int gmax = max((G.g[0] + G.sx - 1) / G.sx, max(G.g[1], G.g[2]));
   for (int e = wave; e < n; e += nwaves) {
     const size_t q = (size_t)L_.slow_q[e];
     double thr = L_.slow_thr[e];
@@ -2305,12 +2317,7 @@ __global__ __launch_bounds__(256) void k_knn_slow(
     int R = -1;
     if (thr < INFINITY) {
       for (int r = 1; r <= kSlowMaxR; ++r) {
-        double L = INFINITY;
-#pragma unroll
-        for (int a = 0; a < 3; ++a) {
-          if (c[a] - r > 0) L = fmin(L, qv[a] - (G.o[a] + (c[a] - r) * G.h));
-          if (c[a] + r < G.g[a] - 1) L = fmin(L, (G.o[a] + (c[a] + r + 1) * G.h) - qv[a]);
-        }
+        const double L = block_reach(G, qv, c, r);
         const double Lg = L - 2.0 * G.delta;
         if (L == INFINITY || (Lg > 0.0 && thr < Lg * Lg)) {
           R = r;
@@ -2319,7 +2326,7 @@ __global__ __launch_bounds__(256) void k_knn_slow(
       }
     }
     if (R > 0) {
-      const int xl = max(c[0] - R, 0), xh = min(c[0] + R, G.g[0] - 1);
+      const int xl = max(c[0] - R * G.sx, 0), xh = min(c[0] + R * G.sx, G.g[0] - 1);
       const int yl = max(c[1] - R, 0), yh = min(c[1] + R, G.g[1] - 1);
       const int zl = max(c[2] - R, 0), zh = min(c[2] + R, G.g[2] - 1);
       const int ny = yh - yl + 1, nrows = ny * (zh - zl + 1);  // <= 49
@@ -2398,15 +2405,17 @@ __global__ __launch_bounds__(256) void k_knn_slow(
       knn_wave_merge<K>(kd, ki, md, mi, lane);
     }
     for (int r = 0; R < 0 && r <= gmax; ++r) {
-      // the ring's cube clipped to the grid (a degenerate axis stays 1 thick)
-      const int xl = max(c[0] - r, 0), xh = min(c[0] + r, G.g[0] - 1);
+      // the ring's cube clipped to the grid (a degenerate axis stays 1 thick);
+      // x reaches r * sx cells
+      const int xl = max(c[0] - r * G.sx, 0), xh = min(c[0] + r * G.sx, G.g[0] - 1);
       const int yl = max(c[1] - r, 0), yh = min(c[1] + r, G.g[1] - 1);
       const int zl = max(c[2] - r, 0), zh = min(c[2] + r, G.g[2] - 1);
       const int bx = xh - xl + 1, by = yh - yl + 1, bz = zh - zl + 1;
       const int nbox = bx * by * bz;
       for (int u = lane; u < nbox; u += kWave) {
         const int x = xl + u % bx, y = yl + (u / bx) % by, z = zl + u / (bx * by);
-        if (max(abs(x - c[0]), max(abs(y - c[1]), abs(z - c[2]))) != r) continue;
+        if (max((abs(x - c[0]) + G.sx - 1) / G.sx, max(abs(y - c[1]), abs(z - c[2]))) != r)
+          continue;
         if (box_d2(G, qv, x, x, y, y, z, z) > thr) continue;
         const int cell = (z * G.g[1] + y) * G.g[0] + x;
         const int b = start[cell], en = start[cell + 1];
@@ -2424,12 +2433,7 @@ __global__ __launch_bounds__(256) void k_knn_slow(
         thr = fmin(thr, md[K - 1] * md[K - 1] * (1.0 + 0x1p-46));
         thr_f = f32_bound(thr, dl);
       }
-      double L = INFINITY;
-#pragma unroll
-      for (int a = 0; a < 3; ++a) {
-        if (c[a] - r > 0) L = fmin(L, qv[a] - (G.o[a] + (c[a] - r) * G.h));
-        if (c[a] + r < G.g[a] - 1) L = fmin(L, (G.o[a] + (c[a] + r + 1) * G.h) - qv[a]);
-      }
+      const double L = block_reach(G, qv, c, r);
       if (L == INFINITY) break;
       const double Lg = L - 2.0 * G.delta;
       if (Lg > 0.0 && thr < Lg * Lg) break;  // all points with dsq <= thr seen
@@ -2459,7 +2463,8 @@ struct navgpu_ctx {
   int tan_R = -1, tan_C = -1;
   hipStream_t aux = nullptr;                 // side stream (pair path: curvature)
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
-  double knn_occ = 5.0;  // target points per grid cell (NAVGPU_KNN_OCC)
+  double knn_occ = 5.0;  // target points per h^3 grid cell (NAVGPU_KNN_OCC)
+  int knn_sx = NAVGPU_KNN_SX;  // x cells per h (NAVGPU_KNN_SX)
   int knn_blocks = 0;    // k_knn blocks per XCD, 0 = auto (NAVGPU_KNN_BLOCKS)
   bool knn_stats = false;
 };
@@ -2607,6 +2612,10 @@ int navgpu_create(int device, void *stream, navgpu_ctx **out) {
   c->device = device;
   if (const char *st = getenv("NAVGPU_KNN_STATS")) c->knn_stats = *st && *st != '0';
   if (const char *o = getenv("NAVGPU_KNN_BLOCKS")) c->knn_blocks = atoi(o);
+  if (const char *o = getenv("NAVGPU_KNN_SX")) {
+    const int v = atoi(o);
+    if (v >= 1 && v <= kMaxSx) c->knn_sx = v;
+  }
   if (const char *o = getenv("NAVGPU_KNN_OCC")) {
     const double v = atof(o);
     if (v > 0.05 && v < 1000) c->knn_occ = v;
@@ -2727,6 +2736,16 @@ long long navgpu_knn_fallbacks(navgpu_ctx *ctx) {
   if (hipStreamSynchronize(ctx->stream) != hipSuccess) return -1;
   if (hipMemcpy(v, it->second.first, 8, hipMemcpyDeviceToHost) != hipSuccess) return -1;
   return (long long)v[1];
+}
+
+long long navgpu_knn_overflows(navgpu_ctx *ctx) {
+  if (!ctx) return -1;
+  auto it = ctx->bufs.find(kStats);
+  if (it == ctx->bufs.end() || !it->second.first) return -1;
+  int v[2] = {0, 0};
+  if (hipStreamSynchronize(ctx->stream) != hipSuccess) return -1;
+  if (hipMemcpy(v, it->second.first, 8, hipMemcpyDeviceToHost) != hipSuccess) return -1;
+  return (long long)v[0];
 }
 
 int navgpu_timing_count(navgpu_ctx *ctx, const char *name) {
@@ -3081,7 +3100,8 @@ static int knn_run(navgpu_ctx *ctx, const double *tgt, size_t nt, const double *
   if (!nq) return NAVGPU_OK;
   ARG_CHECK(queries && idx && dist && (tgt || nt == 0));
   const double occ = ctx->knn_occ;
-  const long long capl = (long long)((double)nt / occ) * 2 + 1024;
+  const int sx = ctx->knn_sx;
+  const long long capl = (long long)((double)nt / occ) * 2 * sx + 1024;
   ARG_CHECK(capl < INT32_MAX / 2);
   const int cap = (int)capl;
   const int nscan = cap + 1;  // start[] has one entry past the last cell
@@ -3156,7 +3176,7 @@ static int knn_run(navgpu_ctx *ctx, const double *tgt, size_t nt, const double *
       CHECK_LAUNCH("k_bbox_partial");
     }
     hipLaunchKernelGGL(k_grid_params, dim3(1), dim3(256), 0, s, part, nt ? nparts : 0, nt,
-                       cap, occ, nq, gp, counters);
+                       cap, occ, sx, nq, gp, counters);
     CHECK_LAUNCH("k_grid_params");
     const dim3 gb(J.s[0].nblk + J.s[1].nblk);
     hipLaunchKernelGGL(k_bin_hist, gb, dim3(256), 0, s, J, gp, tab);

@@ -66,6 +66,7 @@ def _declare(L):
         "navgpu_timing_read": (C.c_double, [_vp, C.c_char_p, C.c_int]),
         "navgpu_timing_count": (C.c_int, [_vp, C.c_char_p]),
         "navgpu_knn_fallbacks": (C.c_longlong, [_vp]),
+        "navgpu_knn_overflows": (C.c_longlong, [_vp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -156,6 +157,11 @@ class NavGpu:
         """Queries of the last knn call that took the exact slow path (-1 if
         not recorded; set NAVGPU_KNN_STATS=1 before creating the context)."""
         return self.L.navgpu_knn_fallbacks(self.h)
+
+    def knn_overflows(self):
+        """k_knn tiles of the last knn call that overflowed the LDS tile and
+        ran from global memory."""
+        return self.L.navgpu_knn_overflows(self.h)
 
     def timing_read(self, name, reset=True):
         n = self.L.navgpu_timing_count(self.h, name.encode())

@@ -32,6 +32,7 @@ dst = torch.empty((N, a.k), dtype=torch.float64, device=dev)
 g.knn_dev(tgt, N, src, N, a.k, idx, dst)
 torch.cuda.synchronize()
 slow = g.knn_fallbacks()
+ovf = g.knn_overflows() if hasattr(g.L, "navgpu_knn_overflows") else -1
 g.timing(True)
 for _ in range(a.reps):
     g.knn_dev(tgt, N, src, N, a.k, idx, dst)
@@ -51,4 +52,4 @@ if hasattr(g.L, "navgpu_debug_stamps") and g.L.navgpu_debug_stamps(st) == 0:
 b_ms, bn = g.timing_read("knn_build")
 print(json.dumps({"lib": os.path.basename(a.lib or "libnavgpu.so"), "occ": float(a.occ), "k": a.k, "query_us": 1000 * q_ms / qn,
                   "build_us": 1000 * b_ms / bn, "slow_lanes": slow,
-                  "slow_frac": slow / N, "stamps": stamps}))
+                  "slow_frac": slow / N, "ovf_chunks": ovf, "stamps": stamps}))
