@@ -1817,20 +1817,23 @@ __device__ __forceinline__ void knn_one(
     B = fmin(B, V - err);
   }
   bool ok = !overflow && Dq < 1e17;
-  // exact f64 re-evaluation of the K+1 survivors. All loads are issued
+  // exact f64 re-evaluation of the K best keys. All loads are issued
   // unconditionally (an empty slot re-reads slot 0) so their latencies
-  // overlap; coordinates come from the cell-sorted copy (L2-local).
-  double ed[KL];
-  int ei[KL];
+  // overlap; coordinates come from the cell-sorted copy (L2-local). The
+  // (K+1)-th key V is the smallest of every candidate left out, so B above
+  // bounds them all: a left-out candidate nearer than the K-th cannot pass
+  // the certificate, and V's own exact distance is never needed.
+  double ed[K];
+  int ei[K];
 #ifdef NAVGPU_DBG_NOEXACT
   if (false) {
 #else
   if (key[0] != kNoKey) {
 #endif
-    int gpos[KL];
-    bool val[KL];
+    int gpos[K];
+    bool val[K];
 #pragma unroll
-    for (int s = 0; s < KL; ++s) {
+    for (int s = 0; s < K; ++s) {
       val[s] = key[s] != kNoKey;
       const int l = (int)((val[s] ? key[s] : key[0]) & kKeyMask);
 #ifdef NAVGPU_DBG_NODECODE  // timing-only ablation: every slot decodes in run 0
@@ -1846,7 +1849,7 @@ __device__ __forceinline__ void knn_one(
       gpos[s] = fgpos(p);
     }
 #pragma unroll
-    for (int s = 0; s < KL; ++s) {
+    for (int s = 0; s < K; ++s) {
 #ifdef NAVGPU_DBG_NOF64  // timing-only ablation: f32 key as the distance
       const double dsq = (double)__uint_as_float(key[s] & ~kKeyMask) + gpos[s] * 1e-30;
       ei[s] = val[s] ? gpos[s] : -1;
@@ -1871,7 +1874,7 @@ __device__ __forceinline__ void knn_one(
 
   } else {
 #pragma unroll
-    for (int s = 0; s < KL; ++s) {
+    for (int s = 0; s < K; ++s) {
       ed[s] = INFINITY;
       ei[s] = -1;
     }
@@ -1879,26 +1882,26 @@ __device__ __forceinline__ void knn_one(
   // order by (distance, index): the truncated-key order is almost always
   // right, and a misordered survivor sits next to its place. Bubble passes
   // run until no lane of the wave is out of order, usually one: some lane of
-  // a wave is misordered about every other batch, so a fixed KL-1 passes
+  // a wave is misordered about every other batch, so a fixed K-1 passes
   // cost a large share of the scan (NAVGPU_SORT_FIXED restores them).
   bool sorted = true;
 #pragma unroll
-  for (int s = 1; s < KL; ++s) sorted &= !knn_less(ed[s], ei[s], ed[s - 1], ei[s - 1]);
+  for (int s = 1; s < K; ++s) sorted &= !knn_less(ed[s], ei[s], ed[s - 1], ei[s - 1]);
 #if defined(NAVGPU_DBG_NOSORT)  // timing-only ablation: no ordering pass
   if (false) {
 #pragma unroll 1
-    for (int pass = 0; pass < KL - 1; ++pass) {
+    for (int pass = 0; pass < K - 1; ++pass) {
 #elif defined(NAVGPU_SORT_FIXED)
   if (!sorted) {
 #pragma unroll 1
-    for (int pass = 0; pass < KL - 1; ++pass) {
+    for (int pass = 0; pass < K - 1; ++pass) {
 #else
   {
 #pragma unroll 1
-    for (int pass = 0; pass < KL - 1 && __any(!sorted); ++pass) {
+    for (int pass = 0; pass < K - 1 && __any(!sorted); ++pass) {
 #endif
 #pragma unroll
-      for (int u = 1; u < KL; ++u) {
+      for (int u = 1; u < K; ++u) {
         const bool sw = knn_less(ed[u], ei[u], ed[u - 1], ei[u - 1]);
         const double td = ed[u];
         const int ti = ei[u];
@@ -1910,7 +1913,7 @@ __device__ __forceinline__ void knn_one(
 #ifndef NAVGPU_SORT_FIXED
       sorted = true;
 #pragma unroll
-      for (int s = 1; s < KL; ++s) sorted &= !knn_less(ed[s], ei[s], ed[s - 1], ei[s - 1]);
+      for (int s = 1; s < K; ++s) sorted &= !knn_less(ed[s], ei[s], ed[s - 1], ei[s - 1]);
 #endif
     }
   }
