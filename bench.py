@@ -525,6 +525,7 @@ def main():
         # matches = feature queries actually searched (constant per pair)
         step()
         torch.cuda.synchronize()
+        tie_rows = g.rows_tie_rows()  # rows that needed the reference tree
         matches_per_step = 0
         if pairs:
             matches_per_step = int((sm[:nd] == 1).sum().item()) * (pairs // nd) \
@@ -542,11 +543,13 @@ def main():
         path_kernels = ["rows_match"]
         workload = (f"{'K2' if a.workload == 'k2' else 'K4'}: {pairs} L9-shaped {R}x{Cc} "
                     "scan pair(s) per GPU, per-row mode (slam.c semantics): curvature of both "
-                    "clouds + exact reference KD per target row + 1-NN of every source feature"
+                    "clouds + exact 1-NN of every source feature against its target row (the "
+                    "reference KD semantics; its tree built only for rows with a distance tie)"
                     + (", RCCL all-gather of the match sets (idx + dist, 12 B per cell)"
                        if gather_buf is not None else ""))
         data = "synthetic L9-shaped range images (navslam.synth.l9_pair), fixed seeds"
-        cfg_extra = {"points_per_cloud": N, "k": 1, "pairs_per_gpu": pairs, "mode": "rows"}
+        cfg_extra = {"points_per_cloud": N, "k": 1, "pairs_per_gpu": pairs, "mode": "rows",
+                     "tie_rows": tie_rows, "rows_per_step": pairs * R}
 
     # warmup (grows the workspace, JITs nothing)
     for _ in range(a.warmup):
@@ -639,12 +642,14 @@ def main():
             ach = dom_bytes / (dom_avg_us * 1e-6) / 1e9
             roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
                     "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 5), "traffic": None,
-                    "kernel": "k_rows_match (fused per-row curvature + exact KD build + 1-NN)",
+                    "kernel": ("rows_match: k_curvature (both clouds) + k_rows_screen (exact "
+                               "f64 argmin + runner-up per query) + the tree pass over tied "
+                               "rows only"),
                     "avg_us": round(dom_avg_us, 2), "bytes_per_launch": dom_bytes,
                     "bytes_model": ("28 B/point x 2 clouds + 36 B/query + 24 B/target feature "
                                     "(SURVEY 8d)"),
-                    "note": ("latency-bound: the exact reference KD permutation is a chain of "
-                             "Lomuto partition passes per row (DESIGN.md)")}
+                    "note": ("f64 VALU-bound screen (chunk-box pruned scan); rows with a tie "
+                             "add the latency-bound Lomuto tree build (DESIGN.md)")}
         path = None
         if path_bytes is not None:
             def path_of(tab, label):

@@ -28,6 +28,8 @@
  *                                                     utils/kdtree.c:110-152
  *   navgpu_rows_match_*    the per-row scan-pair composition:
  *                          extract_feature x2 + per-row build + 1-NN
+ *                          (the tree is built only for rows whose queries
+ *                          have a distance tie)
  *   navgpu_knn_*           global-mode k-NN (the reference has k = 1 only;
  *                          ordering = (distance, index))
  */
@@ -202,6 +204,10 @@ long long navgpu_knn_fallbacks(navgpu_ctx *ctx);
 /* Diagnostic: k_knn tiles of the last navgpu_knn_* call whose neighbourhood
  * exceeded the LDS tile budget and ran from global memory (synchronises). */
 long long navgpu_knn_overflows(navgpu_ctx *ctx);
+/* Diagnostic: rows of the last navgpu_rows_match_* call that had a query
+ * with a distance tie and so ran the reference tree (synchronises); -1 when
+ * the last call did not screen (NAVGPU_ROWS_SCREEN=0) or none was made. */
+long long navgpu_rows_tie_rows(navgpu_ctx *ctx);
 
 #ifdef __cplusplus
 }

@@ -704,12 +704,42 @@ __global__ void k_transform(const double *__restrict__ pts, size_t n, Rigid g,
 // ------------------------------------------------- fused per-row K2 kernel
 // Block = one row of a batch of pairs laid out [pair][R][C]; nn_idx is the
 // target's linear index r*C+c within its own pair.
+// tie != nullptr: the tie pass after k_rows_screen. Rows none of whose S
+// screen splits flagged a tie exit at once; the others build the tree and
+// query only the columns the screen left at kTiePending (masks and the other
+// columns are already written).
+constexpr int32_t kTiePending = -2;
+
+__device__ __forceinline__ bool row_has_tie(const int32_t *tie, int r, int S) {
+  int any = 0;
+  for (int s = 0; s < S; ++s) any |= tie[(size_t)r * S + s];
+  return any != 0;
+}
+
+// nn_idx names the reference's answer, a Point (utils/kdtree.c:110-152 returns
+// coordinates): the lowest column among the row's target features
+// bit-identical to the tree node found at position pos (duplicates, e.g.
+// no-return points at the origin, are otherwise told apart by visit order).
+__device__ __forceinline__ int canon_col(const double *TX, const double *TY, const double *TZ,
+                                         const uint16_t *T, int n, int pos) {
+  const long long rx = __double_as_longlong(TX[pos]), ry = __double_as_longlong(TY[pos]),
+                  rz = __double_as_longlong(TZ[pos]);
+  int best = T[pos];
+  for (int p = 0; p < n; ++p)
+    if (__double_as_longlong(TX[p]) == rx && __double_as_longlong(TY[p]) == ry &&
+        __double_as_longlong(TZ[p]) == rz)
+      best = min(best, (int)T[p]);
+  return best;
+}
+
 __global__ __launch_bounds__(kRowsBlock) void k_rows_match(
     const double *__restrict__ src, const double *__restrict__ tgt, int R,
     int C, int32_t *__restrict__ src_mask, int32_t *__restrict__ tgt_mask,
-    int32_t *__restrict__ nn_idx, double *__restrict__ nn_dist) {
+    int32_t *__restrict__ nn_idx, double *__restrict__ nn_dist,
+    const int32_t *__restrict__ tie, int S) {
   const RowsLds L = rows_lds(C, kRowsBlock, true);
   const int r = blockIdx.x;
+  if (tie && !row_has_tie(tie, r, S)) return;  // uniform
   const size_t rowoff = (size_t)r * C;
   const int pair_row0 = (r % R) * C;  // this row's offset within its pair
   const int n = row_stage_and_build(tgt, tgt, r, C, L, tgt_mask);
@@ -737,9 +767,9 @@ __global__ __launch_bounds__(kRowsBlock) void k_rows_match(
   __syncthreads();
   for (int j = threadIdx.x; j < C; j += blockDim.x) {
     const int f = row_curv_lds(sraw, C, j) > 0.1 ? 1 : 0;
-    SM[j] = (uint16_t)f;
+    SM[j] = (uint16_t)(f && (!tie || nn_idx[rowoff + j] == kTiePending));
     if (src_mask) src_mask[rowoff + j] = f;
-    if (!f) {
+    if (!f && !tie) {
       nn_idx[rowoff + j] = -1;
       nn_dist[rowoff + j] = INFINITY;
     }
@@ -760,7 +790,7 @@ __global__ __launch_bounds__(kRowsBlock) void k_rows_match(
     kd_query(TX, TY, TZ, n, sraw[3 * c], sraw[3 * c + 1], sraw[3 * c + 2],
              stk + threadIdx.x, blockDim.x, &bpos, &bd);
 #endif
-    nn_idx[rowoff + c] = bpos >= 0 ? pair_row0 + (int)T[bpos] : -1;
+    nn_idx[rowoff + c] = bpos >= 0 ? pair_row0 + canon_col(TX, TY, TZ, T, n, bpos) : -1;
     nn_dist[rowoff + c] = bd;
   }
 }
@@ -791,9 +821,11 @@ template <int NT>
 __global__ __launch_bounds__(NT) void k_rows_match_lean(
     const double *__restrict__ src, const double *__restrict__ tgt, int R,
     int C, int32_t *__restrict__ src_mask, int32_t *__restrict__ tgt_mask,
-    int32_t *__restrict__ nn_idx, double *__restrict__ nn_dist) {
+    int32_t *__restrict__ nn_idx, double *__restrict__ nn_dist,
+    const int32_t *__restrict__ tie, int S) {
   constexpr int kHold = kLeanMaxC / NT;
   const int r = blockIdx.x;
+  if (tie && !row_has_tie(tie, r, S)) return;  // uniform
   const size_t rowoff = (size_t)r * C;
   const int pair_row0 = (r % R) * C;
   double *FC = (double *)smem;
@@ -852,9 +884,9 @@ __global__ __launch_bounds__(NT) void k_rows_match_lean(
   const double *sg = src + 3 * rowoff;
   for (int j = threadIdx.x; j < C; j += NT) {
     const int f = row_feature_global(sg, C, j);
-    P[j] = (uint16_t)f;
+    P[j] = (uint16_t)(f && (!tie || nn_idx[rowoff + j] == kTiePending));
     if (src_mask) src_mask[rowoff + j] = f;
-    if (!f) {
+    if (!f && !tie) {
       nn_idx[rowoff + j] = -1;
       nn_dist[rowoff + j] = INFINITY;
     }
@@ -871,9 +903,303 @@ __global__ __launch_bounds__(NT) void k_rows_match_lean(
     double bd;
     kd_query(TX, TY, TZ, n, sg[3 * c], sg[3 * c + 1], sg[3 * c + 2], stk + threadIdx.x, NT,
              &bpos, &bd);
-    nn_idx[rowoff + c] = bpos >= 0 ? pair_row0 + (int)T[bpos] : -1;
+    nn_idx[rowoff + c] = bpos >= 0 ? pair_row0 + canon_col(TX, TY, TZ, T, n, bpos) : -1;
     nn_dist[rowoff + c] = bd;
   }
+}
+
+// ------------------------------------------ per-row screen (K2/K4 batches)
+// nearestNeighborSearch (utils/kdtree.c:110-152) returns a point of minimum
+// reference distance: it skips a far subtree only when |q[a] - node[a]| >=
+// best (kdtree.c:147), and every point beyond the node's plane has a computed
+// distance >= that difference (rounding is monotone, and sqrt(RN(d*d)) = |d|
+// while d*d does not underflow). So when ONE point attains the minimum (no
+// other at the same distance as the reference compares them, after sqrt), the
+// answer does not depend on the tree at all: it is the argmin.
+// The screen finds the minimum and the runner-up of the reference dsq by an
+// exact f64 scan over the row's target features, in 32-point chunks with
+// bounding boxes: a wave skips a chunk when no lane's runner-up could change.
+// A query whose runner-up has the minimum's sqrt (a tie the tree would break
+// by visit order), or whose minimum is a positive distance below 1e-150
+// (d*d underflows there and the argument above fails), is left at
+// kTiePending and its split flags the row; the tie pass (k_rows_match /
+// k_rows_match_lean with `tie`) builds the reference tree for those rows only.
+// Masks come from k_curvature; tie[r*S + split] is written by every split.
+constexpr int kScreenChunk = 32;
+
+__host__ __device__ inline int rows_screen_lds(int C, int w) {
+  const int cp = (C + kScreenChunk - 1) / kScreenChunk * kScreenChunk;
+  return 3 * align16(8 * cp) + 2 * align16(2 * C) + align16(48 * (cp / kScreenChunk)) +
+         align16(2 * w) + align16(4 * 160);
+}
+
+// Stable compaction of columns [c0, c1) with mask[j] != 0, coalesced: thread
+// t takes columns j0 + u NT + t, a wave's ranks come from its ballot, and the
+// (pass, wave) counts are scanned in LDS, so ranks follow column order
+// (flattenPoints, src/slam.c:64-72). U passes are loaded before any is
+// ranked. Writes put(j, rank, load(j)) for each kept column and, when rank_at != null,
+// rank_at[j] = the number of kept columns before j (every j in [c0, c1)).
+// cnt: LDS, >= U * NT / 64 + 1 ints. Returns the count; synchronises.
+template <int NT, class Load, class Put>
+__device__ int compact_cols(int c0, int c1, const int32_t *__restrict__ mask, Load load,
+                            Put put, uint16_t *rank_at, int *cnt) {
+  using Val = decltype(load(0));
+  constexpr int NW = NT / kWave, U = 4;
+  const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
+  int base = 0;
+  for (int j0 = c0; j0 < c1; j0 += U * NT) {
+    bool f[U];
+    unsigned long long bal[U];
+    Val v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int j = j0 + u * NT + (int)threadIdx.x;
+      f[u] = j < c1 && mask[j] != 0;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {  // the kept columns' loads, all in flight
+      const int j = j0 + u * NT + (int)threadIdx.x;
+      if (f[u]) v[u] = load(j);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      bal[u] = __ballot(f[u]);
+      if (lane == 0) cnt[u * NW + wid] = __popcll(bal[u]);
+    }
+    __syncthreads();
+    if (threadIdx.x < kWave) {  // one wave scans the U * NW counts
+      int a = base;
+      for (int i0 = 0; i0 < U * NW; i0 += kWave) {
+        const int i = i0 + lane;
+        const int v = i < U * NW ? cnt[i] : 0;
+        int incl = v;
+#pragma unroll
+        for (int o = 1; o < kWave; o <<= 1) {
+          const int t = __shfl_up(incl, o, kWave);
+          if (lane >= o) incl += t;
+        }
+        if (i < U * NW) cnt[i] = a + incl - v;
+        a += __shfl(incl, kWave - 1, kWave);
+      }
+      if (lane == 0) cnt[U * NW] = a;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int j = j0 + u * NT + (int)threadIdx.x;
+      const int rk = cnt[u * NW + wid] + lanes_below(bal[u]);
+      if (rank_at && j < c1) rank_at[j] = (uint16_t)rk;
+      if (f[u]) put(j, rk, v[u]);
+    }
+    base = cnt[U * NW];
+    __syncthreads();
+  }
+  return base;
+}
+
+template <int NT>
+__global__ __launch_bounds__(NT) void k_rows_screen(
+    const double *__restrict__ src, const double *__restrict__ tgt, int R, int C,
+    const int32_t *__restrict__ src_mask, const int32_t *__restrict__ tgt_mask,
+    int32_t *__restrict__ nn_idx, double *__restrict__ nn_dist, int32_t *__restrict__ tie) {
+  const int r = blockIdx.x, S = gridDim.y, sp = blockIdx.y;
+  const int w = (C + S - 1) / S;
+  const int c0 = sp * w, c1 = min(C, c0 + w);
+  const size_t rowoff = (size_t)r * C;
+  const int pair_row0 = (r % R) * C;
+  const int cp = (C + kScreenChunk - 1) / kScreenChunk * kScreenChunk;
+  double *TX = (double *)smem;
+  double *TY = (double *)(smem + align16(8 * cp));
+  double *TZ = (double *)(smem + 2 * align16(8 * cp));
+  uint16_t *FCOL = (uint16_t *)(smem + 3 * align16(8 * cp));
+  uint16_t *RANK = (uint16_t *)(smem + 3 * align16(8 * cp) + align16(2 * C));
+  double *BOX = (double *)(smem + 3 * align16(8 * cp) + 2 * align16(2 * C));
+  uint16_t *QL = (uint16_t *)((unsigned char *)BOX + align16(48 * (cp / kScreenChunk)));
+  int *scan = (int *)((unsigned char *)QL + align16(2 * w));
+  NV_STAMP(ss0);
+  // target row features, compacted in column order (flattenPoints);
+  // RANK[j] = features before column j
+  const double *tg = tgt + 3 * rowoff;
+  const int n = compact_cols<NT>(
+      0, C, tgt_mask + rowoff, [&](int j) { return double3{tg[3 * j], tg[3 * j + 1], tg[3 * j + 2]}; },
+      [&](int j, int pos, const double3 &p) {
+        TX[pos] = p.x;
+        TY[pos] = p.y;
+        TZ[pos] = p.z;
+        FCOL[pos] = (uint16_t)j;
+      },
+      RANK, scan);
+  NV_STAMP(ss1);
+  NV_STAMP_ADD(0, ss0, ss1);
+  const int nch = (n + kScreenChunk - 1) / kScreenChunk;
+  // the last chunk's tail: +inf coordinates, dsq = inf is never taken
+  for (int e = n + (int)threadIdx.x; e < nch * kScreenChunk; e += NT)
+    TX[e] = TY[e] = TZ[e] = INFINITY;
+  // chunk bounding boxes (NaN coordinates left out: such a point's distance
+  // is NaN and never taken); two chunks per wave per pass, one per half-wave
+  const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
+  constexpr int NW = NT / kWave;
+  for (int b0 = 2 * wid; b0 < nch; b0 += 2 * NW) {
+    const int b = b0 + (lane >> 5), e = b * kScreenChunk + (lane & 31);
+    const bool in = b < nch && e < n;
+    double lo[3], hi[3];
+    const double v[3] = {in ? TX[e] : NAN, in ? TY[e] : NAN, in ? TZ[e] : NAN};
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+      const bool ok = v[a] == v[a];
+      lo[a] = ok ? v[a] : INFINITY;
+      hi[a] = ok ? v[a] : -INFINITY;
+    }
+#pragma unroll
+    for (int o = 16; o > 0; o >>= 1) {
+#pragma unroll
+      for (int a = 0; a < 3; ++a) {
+        lo[a] = fmin(lo[a], __shfl_xor(lo[a], o, kWave));
+        hi[a] = fmax(hi[a], __shfl_xor(hi[a], o, kWave));
+      }
+    }
+    if (b < nch && (lane & 31) == 0) {
+      double *bx = BOX + 6 * b;
+      bx[0] = lo[0];
+      bx[1] = hi[0];
+      bx[2] = lo[1];
+      bx[3] = hi[1];
+      bx[4] = lo[2];
+      bx[5] = hi[2];
+    }
+  }
+  NV_STAMP(ss2);
+  NV_STAMP_ADD(1, ss1, ss2);
+  // this split's source features (block_compact synchronises, so the boxes
+  // and the padded tail are visible after it)
+  const int32_t *sm = src_mask + rowoff;
+  const int nq = compact_cols<NT>(
+      c0, c1, sm, [&](int) { return 0; }, [&](int j, int pos, int) { QL[pos] = (uint16_t)j; },
+      nullptr, scan);
+  for (int j = c0 + (int)threadIdx.x; j < c1; j += NT)
+    if (!sm[j]) {
+      nn_idx[rowoff + j] = -1;
+      nn_dist[rowoff + j] = INFINITY;
+    }
+  int mytie = 0;
+  NV_STAMP(ss3);
+  NV_STAMP_ADD(2, ss2, ss3);
+  for (int i0 = wid * kWave; i0 < nq; i0 += NT) {  // wave-uniform trip count
+    const int i = i0 + lane;
+    const bool act = i < nq;
+    NV_STAMP_ADD(14, 0ull, 1ull);
+    const int c = QL[act ? i : i0];
+    const double *qp = src + 3 * (rowoff + c);
+    const double qx = qp[0], qy = qp[1], qz = qp[2];
+    // start at the chunk holding the first target feature at or after the
+    // wave's first query column (scan rows are azimuth sweeps: the nearest
+    // point is usually a few columns away), then alternate outwards
+    const int s = min((int)RANK[QL[i0]] / kScreenChunk, max(nch - 1, 0));
+    double d1 = INFINITY, d2 = INFINITY;
+    int j1 = -1;
+    auto scan_chunk = [&](int k) {
+      NV_STAMP_ADD(13, 0ull, 1ull);
+      const int e0 = k * kScreenChunk;
+#pragma unroll 8
+      for (int u = 0; u < kScreenChunk; ++u) {
+        const int e = e0 + u;
+        const double dx = TX[e] - qx, dy = TY[e] - qy, dz = TZ[e] - qz;
+        const double d = dx * dx + dy * dy + dz * dz;  // utils/kdtree.c:16
+        j1 = d < d1 ? e : j1;
+        d2 = fmin(d2, fmax(d1, d));  // a NaN d makes d2 = d1: a (safe) tie
+        d1 = fmin(d1, d);
+      }
+    };
+    // lower bound of the computed dsq between any point of box [lo, hi] and
+    // any query of [qlo, qhi] (a single query: qlo = qhi): each |fl(p - q)|
+    // >= fl(gap) by monotone rounding, the same association
+    auto box_lb = [](const double *bx, double qlx, double qhx, double qly, double qhy,
+                     double qlz, double qhz) {
+      const double gx = fmax(fmax(bx[0] - qhx, qlx - bx[1]), 0.0);
+      const double gy = fmax(fmax(bx[2] - qhy, qly - bx[3]), 0.0);
+      const double gz = fmax(fmax(bx[4] - qhz, qlz - bx[5]), 0.0);
+      return gx * gx + gy * gy + gz * gz;
+    };
+    // the two chunks where the wave's columns start (its queries' nearest
+    // points are usually there), unconditionally
+    const int s2 = min(s + 1, nch - 1);
+    if (nch > 0) scan_chunk(s);
+    if (s2 != s) scan_chunk(s2);
+    // then one test per CHUNK, a lane per chunk: the chunk's box against the
+    // box of the wave's queries and the largest runner-up of its lanes; only
+    // chunks that pass get the per-query test and the scan
+    const bool qok = act && qx == qx && qy == qy && qz == qz;  // NaN: never matches
+    double wl[3] = {qok ? qx : INFINITY, qok ? qy : INFINITY, qok ? qz : INFINITY};
+    double wh[3] = {qok ? qx : -INFINITY, qok ? qy : -INFINITY, qok ? qz : -INFINITY};
+    double wd2 = qok ? d2 : -INFINITY;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+#pragma unroll
+      for (int a = 0; a < 3; ++a) {
+        wl[a] = fmin(wl[a], __shfl_xor(wl[a], o, kWave));
+        wh[a] = fmax(wh[a], __shfl_xor(wh[a], o, kWave));
+      }
+      wd2 = fmax(wd2, __shfl_xor(wd2, o, kWave));
+    }
+    for (int k0 = 0; k0 < nch; k0 += kWave) {
+      const int kl = k0 + lane;
+      bool pass = false;
+      if (kl < nch && kl != s && kl != s2)
+        pass = box_lb(BOX + 6 * kl, wl[0], wh[0], wl[1], wh[1], wl[2], wh[2]) <= wd2;
+      unsigned long long m = __ballot(pass);
+      while (m) {
+        const int k = k0 + __builtin_ctzll(m);
+        m &= m - 1;
+        const double lb = box_lb(BOX + 6 * k, qx, qx, qy, qy, qz, qz);
+        if (__any(act && lb <= d2)) scan_chunk(k);
+      }
+    }
+    const double dist = __builtin_sqrt(d1);
+    // a runner-up at the minimum's distance: a real tie only if some point
+    // in that distance band has other coordinates (the reference returns a
+    // Point, so bit-identical duplicates give the same answer whichever the
+    // tree visits first; nn_idx then names the lowest column among them).
+    // Rare (duplicated no-return points at the origin, integer data), so it
+    // is a second pass over the chunks that can hold the band.
+    const bool suspect = act && d1 < INFINITY && __builtin_sqrt(d2) == dist;
+    bool genuine = false;
+    int emin = j1;
+    if (__any(suspect)) {
+      const int jr = j1 >= 0 ? j1 : 0;
+      const long long rx = __double_as_longlong(TX[jr]), ry = __double_as_longlong(TY[jr]),
+                      rz = __double_as_longlong(TZ[jr]);
+      for (int k = 0; k < nch; ++k) {
+        const double lb = box_lb(BOX + 6 * k, qx, qx, qy, qy, qz, qz);
+        if (!__any(suspect && __builtin_sqrt(lb) <= dist)) continue;
+        for (int u = 0; u < kScreenChunk; ++u) {
+          const int e = k * kScreenChunk + u;
+          const double dx = TX[e] - qx, dy = TY[e] - qy, dz = TZ[e] - qz;
+          const double d = dx * dx + dy * dy + dz * dz;
+          if (suspect && __builtin_sqrt(d) == dist) {
+            const bool same = __double_as_longlong(TX[e]) == rx &&
+                              __double_as_longlong(TY[e]) == ry &&
+                              __double_as_longlong(TZ[e]) == rz;
+            genuine |= !same;
+            emin = same ? min(emin, e) : emin;
+          }
+        }
+      }
+    }
+    if (act) {
+      const bool t = genuine || (d1 < INFINITY && dist > 0.0 && dist < 1e-150);
+      if (t) {
+        nn_idx[rowoff + c] = kTiePending;
+        mytie = 1;
+      } else {
+        nn_idx[rowoff + c] = j1 >= 0 ? pair_row0 + (int)FCOL[emin] : -1;
+        nn_dist[rowoff + c] = j1 >= 0 ? dist : INFINITY;
+      }
+    }
+  }
+  NV_STAMP(ss4);
+  NV_STAMP_ADD(3, ss3, ss4);
+  const int any = __syncthreads_or(mytie);
+  if (threadIdx.x == 0) tie[(size_t)r * S + sp] = any;
 }
 
 // ------------------------------------------- split per-row build / query
@@ -2470,6 +2796,7 @@ struct navgpu_ctx {
   int knn_sx = NAVGPU_KNN_SX;  // x cells per h (NAVGPU_KNN_SX)
   int knn_blocks = 0;    // k_knn blocks per XCD, 0 = auto (NAVGPU_KNN_BLOCKS)
   bool knn_stats = false;
+  int screen_rows = 0, screen_S = 0;  // last screened rows_match call (tie diagnostic)
 };
 
 namespace {
@@ -2477,7 +2804,7 @@ namespace {
 enum Slot {
   kBBox = 1, kParams, kCnt, kStart, kBSum, kCellId, kSlotBuf, kRec, kTan,
   kKdFc, kKdP, kKdT, kQStart, kQCell, kQSlot, kQPerm, kStats, kOvf, kSlowQ,
-  kSlowThr, kTSort,
+  kSlowThr, kTSort, kRowMaskS, kRowMaskT, kRowTie,
   kH0 = 100, kH1, kH2, kH3, kH4, kH5,
 };
 
@@ -2751,6 +3078,23 @@ long long navgpu_knn_overflows(navgpu_ctx *ctx) {
   return (long long)v[0];
 }
 
+long long navgpu_rows_tie_rows(navgpu_ctx *ctx) {
+  if (!ctx || ctx->screen_rows <= 0) return -1;
+  auto it = ctx->bufs.find(kRowTie);
+  if (it == ctx->bufs.end() || !it->second.first) return -1;
+  std::vector<int32_t> v((size_t)ctx->screen_rows * ctx->screen_S);
+  if (hipStreamSynchronize(ctx->stream) != hipSuccess) return -1;
+  if (hipMemcpy(v.data(), it->second.first, 4 * v.size(), hipMemcpyDeviceToHost) != hipSuccess)
+    return -1;
+  long long n = 0;
+  for (int r = 0; r < ctx->screen_rows; ++r) {
+    int any = 0;
+    for (int s = 0; s < ctx->screen_S; ++s) any |= v[(size_t)r * ctx->screen_S + s];
+    n += any != 0;
+  }
+  return n;
+}
+
 int navgpu_timing_count(navgpu_ctx *ctx, const char *name) {
   if (!ctx || !name) return -1;
   auto it = ctx->ev.find(name);
@@ -2941,6 +3285,86 @@ int navgpu_rows_corr_dev(navgpu_ctx *ctx, const double *tree_pts,
   return NAVGPU_OK;
 }
 
+namespace {
+
+// The per-row scan-pair step over `rows` rows ([pair][R][C], R | rows).
+// Default: k_curvature (both masks) -> k_rows_screen (exact argmin per query,
+// ties flagged) -> the tree kernel for flagged rows only. NAVGPU_ROWS_SCREEN=0
+// runs the tree kernel on every row (the r1 path; same results).
+int rows_match_launch(navgpu_ctx *ctx, const double *src, const double *tgt, int rows,
+                      int R, int C, int32_t *src_mask, int32_t *tgt_mask, int32_t *nn_idx,
+                      double *nn_dist) {
+  const char *sc = getenv("NAVGPU_ROWS_SCREEN");
+  const bool screen = !(sc && *sc == '0');
+  // enough rows to fill the chip several times over: the lean tree kernel
+  // (two rows per CU); a short batch keeps the 512-thread one (lower latency)
+  const bool lean = C <= kLeanMaxC && rows >= 1024 && !getenv("NAVGPU_ROWS_NO_LEAN");
+  const int32_t *tie = nullptr;
+  int S = 1;
+  TimedRegion tr(ctx, "rows_match");
+  if (screen) {
+    const size_t N = (size_t)rows * C;
+    if (!src_mask) RC(ws(ctx, kRowMaskS, N, &src_mask));
+    if (!tgt_mask) RC(ws(ctx, kRowMaskT, N, &tgt_mask));
+    // column splits: >= 512 workgroups in all (two per CU: ~64 KB of LDS
+    // each), >= 128 columns each; 512 threads once a split holds >= 512
+    // columns (measured: K2 83 us at S = 4 x 512 threads, 102 us at S = 8 x
+    // 256; a K4 batch is fastest unsplit at 512 threads)
+    while (S < 8 && (long long)rows * S < 512 && C / (2 * S) >= 128) S <<= 1;
+    if (const char *e = getenv("NAVGPU_SCREEN_S")) S = std::max(1, std::min(64, atoi(e)));
+    const int w = (C + S - 1) / S;
+    int32_t *tf;
+    RC(ws(ctx, kRowTie, (size_t)rows * S, &tf));
+    tie = tf;
+    ctx->screen_rows = rows;
+    ctx->screen_S = S;
+    // R1 on both clouds, <= 65535 rows per launch (grid y)
+    for (int r0 = 0; r0 < rows; r0 += 65535) {
+      const int nr = std::min(rows - r0, 65535);
+      const size_t o = (size_t)r0 * C;
+      CurvJob J = {{src + 3 * o, tgt + 3 * o}, {src_mask + o, tgt_mask + o}, {nullptr, nullptr}};
+      hipLaunchKernelGGL(k_curvature, dim3((C + kCurvTile - 1) / kCurvTile, nr, 2),
+                         dim3(kCurvTile), 0, ctx->stream, J, nr, C);
+      CHECK_LAUNCH("k_curvature");
+    }
+    const int lds = rows_screen_lds(C, w);
+    if (lds > lds_limit()) {
+      set_err("rows_screen: C=%d needs %d B of LDS (device limit %d)", C, lds, lds_limit());
+      return NAVGPU_ERANGE;
+    }
+    const char *nte = getenv("NAVGPU_SCREEN_NT");
+    if (nte ? atoi(nte) == 512 : w >= 512) {
+      RC(set_lds(k_rows_screen<512>, lds));
+      hipLaunchKernelGGL(k_rows_screen<512>, dim3(rows, S), dim3(512), lds, ctx->stream, src,
+                         tgt, R, C, src_mask, tgt_mask, nn_idx, nn_dist, tf);
+    } else {
+      RC(set_lds(k_rows_screen<256>, lds));
+      hipLaunchKernelGGL(k_rows_screen<256>, dim3(rows, S), dim3(256), lds, ctx->stream, src,
+                         tgt, R, C, src_mask, tgt_mask, nn_idx, nn_dist, tf);
+    }
+    CHECK_LAUNCH("k_rows_screen");
+    // the tie pass writes no masks (already written)
+    src_mask = nullptr;
+    tgt_mask = nullptr;
+  }
+  if (lean) {
+    const int lds = rows_lean_lds(C, 256);
+    RC(set_lds(k_rows_match_lean<256>, lds));
+    hipLaunchKernelGGL(k_rows_match_lean<256>, dim3(rows), dim3(256), lds, ctx->stream, src,
+                       tgt, R, C, src_mask, tgt_mask, nn_idx, nn_dist, tie, S);
+    CHECK_LAUNCH("k_rows_match_lean");
+    return NAVGPU_OK;
+  }
+  const RowsLds L = rows_lds(C, kRowsBlock, true);
+  RC(set_lds(k_rows_match, L.total));
+  hipLaunchKernelGGL(k_rows_match, dim3(rows), dim3(kRowsBlock), L.total, ctx->stream, src,
+                     tgt, R, C, src_mask, tgt_mask, nn_idx, nn_dist, tie, S);
+  CHECK_LAUNCH("k_rows_match");
+  return NAVGPU_OK;
+}
+
+}  // namespace
+
 int navgpu_rows_match_dev(navgpu_ctx *ctx, const double *src,
                           const double *tgt, int R, int C, int32_t *src_mask,
                           int32_t *tgt_mask, int32_t *nn_idx, double *nn_dist) {
@@ -2948,14 +3372,7 @@ int navgpu_rows_match_dev(navgpu_ctx *ctx, const double *src,
   RC(check_rows_shape(R, C, true));
   if ((size_t)R * C == 0) return NAVGPU_OK;
   ARG_CHECK(src && tgt && nn_idx && nn_dist);
-  const RowsLds L = rows_lds(C, kRowsBlock, true);
-  RC(set_lds(k_rows_match, L.total));
-  TimedRegion tr(ctx, "rows_match");
-  hipLaunchKernelGGL(k_rows_match, dim3(R), dim3(kRowsBlock), L.total,
-                     ctx->stream, src, tgt, R, C, src_mask, tgt_mask, nn_idx,
-                     nn_dist);
-  CHECK_LAUNCH("k_rows_match");
-  return NAVGPU_OK;
+  return rows_match_launch(ctx, src, tgt, R, R, C, src_mask, tgt_mask, nn_idx, nn_dist);
 }
 
 int navgpu_rows_match_batch_dev(navgpu_ctx *ctx, const double *src,
@@ -2967,25 +3384,8 @@ int navgpu_rows_match_batch_dev(navgpu_ctx *ctx, const double *src,
   ARG_CHECK((long long)npairs * R <= INT32_MAX && (long long)npairs * R * C < INT32_MAX);
   if ((size_t)npairs * R * C == 0) return NAVGPU_OK;
   ARG_CHECK(src && tgt && nn_idx && nn_dist);
-  TimedRegion tr(ctx, "rows_match");
-  // enough rows to fill the chip several times over: the lean variant (two
-  // rows per CU); a short batch keeps the 512-thread kernel (lower latency
-  // per row)
-  if (C <= kLeanMaxC && (long long)npairs * R >= 1024 && !getenv("NAVGPU_ROWS_NO_LEAN")) {
-    const int lds = rows_lean_lds(C, 256);
-    RC(set_lds(k_rows_match_lean<256>, lds));
-    hipLaunchKernelGGL(k_rows_match_lean<256>, dim3(npairs * R), dim3(256), lds, ctx->stream,
-                       src, tgt, R, C, src_mask, tgt_mask, nn_idx, nn_dist);
-    CHECK_LAUNCH("k_rows_match_lean");
-    return NAVGPU_OK;
-  }
-  const RowsLds L = rows_lds(C, kRowsBlock, true);
-  RC(set_lds(k_rows_match, L.total));
-  hipLaunchKernelGGL(k_rows_match, dim3(npairs * R), dim3(kRowsBlock), L.total,
-                     ctx->stream, src, tgt, R, C, src_mask, tgt_mask, nn_idx,
-                     nn_dist);
-  CHECK_LAUNCH("k_rows_match");
-  return NAVGPU_OK;
+  return rows_match_launch(ctx, src, tgt, npairs * R, R, C, src_mask, tgt_mask, nn_idx,
+                           nn_dist);
 }
 
 int navgpu_rows_match_host(navgpu_ctx *ctx, const double *src,

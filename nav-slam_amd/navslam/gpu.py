@@ -67,6 +67,7 @@ def _declare(L):
         "navgpu_timing_count": (C.c_int, [_vp, C.c_char_p]),
         "navgpu_knn_fallbacks": (C.c_longlong, [_vp]),
         "navgpu_knn_overflows": (C.c_longlong, [_vp]),
+        "navgpu_rows_tie_rows": (C.c_longlong, [_vp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -162,6 +163,11 @@ class NavGpu:
         """k_knn tiles of the last knn call that overflowed the LDS tile and
         ran from global memory."""
         return self.L.navgpu_knn_overflows(self.h)
+
+    def rows_tie_rows(self):
+        """Rows of the last rows_match call that had a distance tie and ran
+        the reference tree (-1 if that call did not screen)."""
+        return self.L.navgpu_rows_tie_rows(self.h)
 
     def timing_read(self, name, reset=True):
         n = self.L.navgpu_timing_count(self.h, name.encode())

@@ -277,7 +277,16 @@ void orc_rows_match(const double *src, const double *tgt, int R, int C,
             double d;
             orc_kd_nn(flat, n, src + 3 * g, &pos, &d);
             if (pos >= 0) {
-                nn_idx[g] = r * C + fcol[pos];
+                /* the reference returns the Point (kdtree.c:121); its index
+                 * is the lowest column among the row's features holding
+                 * exactly those coordinates (bitwise), so duplicated points
+                 * name one canonical index whichever the tree visits first */
+                int col = fcol[pos];
+                for (size_t p = 0; p < n; p++)
+                    if (memcmp(flat + 3 * p, flat + 3 * pos, 3 * sizeof(double)) == 0 &&
+                        fcol[p] < col)
+                        col = fcol[p];
+                nn_idx[g] = r * C + col;
                 nn_dist[g] = d;
             }
         }

@@ -190,6 +190,42 @@ def test_rows_match_edge_cases(gpu, orc):
         _eq(gpu.rows_match(c, t)[3], orc.rows_match(c, t)[3], f"dist {c.shape}")
 
 
+def test_rows_screen_vs_tree_path(gpu, orc, monkeypatch):
+    """The screened per-row path (exact argmin, the reference tree only for
+    rows with a tie) == the tree on every row (NAVGPU_ROWS_SCREEN=0) == the
+    oracle, on data that stresses the screen's argument: integer ties,
+    non-finite coordinates, distances whose squares underflow, duplicate
+    points, large offsets (utils/kdtree.c:110-152)."""
+    from navslam.synth import l9_pair
+    rng = np.random.default_rng(77)
+    cases = []
+    src, tgt = l9_pair(32, 512, seed=5)
+    cases.append(("l9 f64", src, tgt))
+    cases.append(("l9 integer", *l9_pair(32, 512, seed=6, integer_mm=True)))
+    s2, t2 = src.copy(), tgt.copy()
+    s2[3, 100:140, 1] = np.nan
+    t2[4, 200:260, 0] = np.inf
+    t2[5, 10:400:7, 2] = np.nan
+    s2[6, 300:340] = -np.inf
+    cases.append(("non-finite", s2, t2))
+    tiny = rng.uniform(0, 1, (4, 256, 3)) * 1e-160
+    cases.append(("tiny", tiny, tiny[:, ::-1].copy() * 1.0000001))
+    dup = np.round(rng.uniform(0, 50, (8, 300, 3)))
+    cases.append(("duplicates", dup, dup[::-1].copy()))
+    off = rng.uniform(0, 100, (8, 700, 3)) + 1e9
+    cases.append(("offset", off, off + rng.uniform(-1, 1, off.shape)))
+    names = ("src_mask", "tgt_mask", "nn_idx", "nn_dist")
+    for label, s, t in cases:
+        monkeypatch.delenv("NAVGPU_ROWS_SCREEN", raising=False)
+        got = gpu.rows_match(s, t)
+        monkeypatch.setenv("NAVGPU_ROWS_SCREEN", "0")
+        tree = gpu.rows_match(s, t)
+        ref = orc.rows_match(s, t)
+        for a, b, c, name in zip(got, tree, ref, names):
+            _eq(a, b, f"{label}: screen vs tree {name}")
+            _eq(a, c, f"{label}: screen vs oracle {name}")
+
+
 def test_split_build_query_vs_oracle(gpu, orc):
     """kd_build_rows_dev + kd_query_rows_dev on device tensors (slam.c split:
     features from the lidar frame, coordinates from a transformed frame)."""
