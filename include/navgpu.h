@@ -131,6 +131,19 @@ int navgpu_rows_corr_dev(navgpu_ctx *ctx, const double *tree_pts,
                          const double *nn_dist, const double *ori, int R, int C,
                          int32_t *keep, double *sums);
 
+/* The bit-exact counterpart: the reference's correspondence list itself
+ * (src/slam.c:235-284), rows in order, each row's entries in first-insertion
+ * order (the column of the first query that found that nearest point), each
+ * entry holding the query kept for it (smallest distance, then first
+ * column). list[7*i .. 7*i+6] = oriPoint (ori at the kept query), nearestPoint,
+ * distance: the NeighborResult layout of utils/kdtree.h. list holds up to
+ * R*C entries; count[0] = entries, count[1] = queries that found a point.
+ * Queries with nn_pos == -1 (no feature, empty row tree) make no entry. */
+int navgpu_rows_corr_list_dev(navgpu_ctx *ctx, const double *tree_pts,
+                              const int32_t *tree_n, const int32_t *nn_pos,
+                              const double *nn_dist, const double *ori, int R, int C,
+                              double *list, int32_t *count);
+
 /* ---- The K2 scan-pair step, per-row mode (fused, one kernel) ------------
  * masks of src and tgt (R1), per-row target trees (R4+R5), every src
  * feature queried against its row's tree (R6). nn_idx = linear target index

@@ -299,7 +299,9 @@ __device__ void wave_nth_element(const double *key, IdxT *P, IdxT *T,
 // positions per step. Small counts are prefix-summed across the waves;
 // tape chains that cross waves are resolved by pointer jumping through LDS
 // (bit 31 = resolved, else the chunk position whose value it equals).
-// Requires blockDim.x <= kBlockNthMax; P/T in LDS.
+// Requires blockDim.x <= kBlockNthMax; P/T in LDS, or in global memory
+// (k_kd_level: every chunk ends at a barrier, which orders the waves'
+// global writes at workgroup scope).
 constexpr int kBlockNthMax = 1024;
 template <class IdxT>
 __device__ void block_nth_element(const double *key, IdxT *P, IdxT *T, int first,
@@ -1315,6 +1317,73 @@ inline int kd_build_lds_bytes(int n) {
   return align16(24 * n) + 2 * align16(2 * n);
 }
 
+// ---- buildKDTree for arrays beyond one workgroup's LDS: level-parallel.
+// k_kd_prep: SoA key copy + identity permutation. k_kd_level: the
+// nth_element of every subarray of one depth, one single-wave workgroup per
+// subarray (2^d of them; the reference's Lomuto passes on global P/T).
+// k_kd_leaves: once every subarray fits the LDS build, one workgroup builds
+// each whole subtree in LDS (root axis = its depth) and writes its points.
+__global__ __launch_bounds__(256) void k_kd_prep(const double *__restrict__ pts, int n,
+                                                 double *__restrict__ FC,
+                                                 uint32_t *__restrict__ P) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (size_t)n) return;
+  FC[i] = pts[3 * i];
+  FC[(size_t)n + i] = pts[3 * i + 1];
+  FC[2 * (size_t)n + i] = pts[3 * i + 2];
+  P[i] = (uint32_t)i;
+}
+
+// pts[i] = point P[i]: places the upper levels' nodes (the leaves kernel
+// then overwrites every leaf subarray with its built subtree)
+__global__ __launch_bounds__(256) void k_kd_gather(double *__restrict__ pts,
+                                                   const double *__restrict__ FC, int n,
+                                                   const uint32_t *__restrict__ P) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (size_t)n) return;
+  const uint32_t e = P[i];
+  pts[3 * i] = FC[e];
+  pts[3 * i + 1] = FC[(size_t)n + e];
+  pts[3 * i + 2] = FC[2 * (size_t)n + e];
+}
+
+__global__ __launch_bounds__(1024) void k_kd_level(const double *__restrict__ FC, int n,
+                                                   int depth0, int d, uint32_t *P,
+                                                   uint32_t *T) {
+  int lo, hi;
+  kd_node_range(n, d, (int)blockIdx.x, lo, hi);
+  if (hi - lo < 2) return;
+  const double *key = FC + (size_t)((depth0 + d) % 3) * n;
+  // the block-wide tape pass on global P/T: 1024 positions per step (the
+  // barriers order the waves' global writes at workgroup scope)
+  block_nth_element<uint32_t>(key, P, T, lo, hi - 1, lo + (hi - lo) / 2);
+}
+
+__global__ __launch_bounds__(1024) void k_kd_leaves(double *__restrict__ pts,
+                                                    const double *__restrict__ FC, int n,
+                                                    int depth0, int L,
+                                                    const uint32_t *__restrict__ P) {
+  int lo, hi;
+  kd_node_range(n, L, (int)blockIdx.x, lo, hi);
+  const int m = hi - lo;
+  if (m <= 0) return;
+  double *lf = (double *)smem;  // SoA, m points
+  uint16_t *Pl = (uint16_t *)(smem + align16(24 * m));
+  uint16_t *Tl = Pl + ((align16(2 * m)) / 2);
+  for (int i = threadIdx.x; i < m; i += blockDim.x) {
+    const uint32_t e = P[lo + i];
+    lf[i] = FC[e];
+    lf[m + i] = FC[(size_t)n + e];
+    lf[2 * m + i] = FC[2 * (size_t)n + e];
+  }
+  __syncthreads();
+  block_build_kdtree<uint16_t>(lf, m, m, Pl, Tl, (depth0 + L) % 3);
+  for (int i = threadIdx.x; i < 3 * m; i += blockDim.x) {
+    const int pos = i / 3, a = i % 3;
+    pts[3 * (size_t)lo + i] = lf[a * m + Pl[pos]];
+  }
+}
+
 // ------------------------------------------------- R7: correspondence dedup
 // src/slam.c:247-284, one workgroup per row: of the row's feature queries
 // that found the same nearest point (coordinate equality, -0.0 == 0.0), the
@@ -1342,13 +1411,15 @@ __global__ __launch_bounds__(kCorrBlock) void k_rows_corr(
     const double *__restrict__ tree_pts, const int32_t *__restrict__ tree_n,
     const int32_t *__restrict__ nn_pos, const double *__restrict__ nn_dist,
     const double *__restrict__ ori, int C, int HS, int32_t *__restrict__ keep,
-    double *__restrict__ sums) {
+    double *__restrict__ sums, double *__restrict__ ent, int32_t *__restrict__ ent_n) {
   extern __shared__ __attribute__((aligned(8))) unsigned char corr_lds[];
   unsigned long long *bdist = (unsigned long long *)corr_lds;  // [HS]
   int *owner = (int *)(bdist + HS);                            // [HS]
   int *bcol = owner + HS;                                      // [HS]
-  int *canon = bcol + HS;                                      // [C]
+  int *fcol = bcol + HS;                                       // [HS] (ent only)
+  int *canon = fcol + HS;                                      // [C]
   __shared__ double red[kCorrBlock / kWave][6];
+  __shared__ int cscan[kCorrBlock / kWave + 1];
   const int row = blockIdx.x;
   const size_t base = (size_t)row * C;
   const int n = tree_n[row];
@@ -1356,6 +1427,7 @@ __global__ __launch_bounds__(kCorrBlock) void k_rows_corr(
     owner[h] = -1;
     bdist[h] = ~0ull;
     bcol[h] = INT_MAX;
+    fcol[h] = INT_MAX;
   }
   __syncthreads();
   // canonical slot of every tree point (-1: a NaN coordinate)
@@ -1385,7 +1457,10 @@ __global__ __launch_bounds__(kCorrBlock) void k_rows_corr(
     const int pos = nn_pos[base + c];
     if (pos < 0 || pos >= n) continue;
     const int h = canon[pos];
-    if (h >= 0) atomicMin(&bdist[h], (unsigned long long)__double_as_longlong(nn_dist[base + c]));
+    if (h >= 0) {
+      atomicMin(&bdist[h], (unsigned long long)__double_as_longlong(nn_dist[base + c]));
+      if (ent) atomicMin(&fcol[h], c);
+    }
   }
   __syncthreads();
   for (int c = threadIdx.x; c < C; c += blockDim.x) {
@@ -1447,8 +1522,64 @@ __global__ __launch_bounds__(kCorrBlock) void k_rows_corr(
     m2 += ex * ex + ey * ey + ez * ez;
   }
   block_sum(&m2, 1);
-  if (threadIdx.x < 6)
+  if (sums && threadIdx.x < 6)
     sums[(size_t)row * 6 + threadIdx.x] = threadIdx.x == 3 ? m2 : acc[threadIdx.x];
+  if (!ent) return;
+  // the row's correspondence list in the reference's order: an entry per
+  // distinct nearest point at its FIRST query's column (src/slam.c:247-281
+  // appends there), holding the KEPT query (smallest distance, then first
+  // column: the in-place replacements leave that one). A NaN point is an
+  // entry of its own. ent[(row*C + rank)*7]: oriPoint, nearestPoint, distance
+  // (the NeighborResult layout, utils/kdtree.h); ent_n[row] = the count.
+  const int ne = block_compact(
+      C, cscan,
+      [&](int c) {
+        const int pos = nn_pos[base + c];
+        if (pos < 0 || pos >= n) return false;
+        const int h = canon[pos];
+        return h < 0 || fcol[h] == c;
+      },
+      [&](int c, int rank) {
+        const int h = canon[nn_pos[base + c]];
+        const int kc = h < 0 ? c : bcol[h];
+        const int kp = nn_pos[base + kc];
+        const double *a = ori + 3 * (base + kc), *b = tree_pts + 3 * (base + kp);
+        double *e = ent + 7 * (base + rank);
+        e[0] = a[0];
+        e[1] = a[1];
+        e[2] = a[2];
+        e[3] = b[0];
+        e[4] = b[1];
+        e[5] = b[2];
+        e[6] = nn_dist[base + kc];
+      });
+  if (threadIdx.x == 0) ent_n[row] = ne;
+}
+
+// Concatenates the rows' lists of k_rows_corr (row order) into list[7 * i];
+// count[0] = entries, count[1] = queries that found a nearest point.
+__global__ __launch_bounds__(256) void k_corr_pack(const double *__restrict__ ent,
+                                                   const int32_t *__restrict__ ent_n,
+                                                   const double *__restrict__ sums, int R,
+                                                   int C, double *__restrict__ list,
+                                                   int32_t *__restrict__ count) {
+  __shared__ int part[256 / kWave + 1];
+  const int row = blockIdx.x;
+  int off = 0;
+  for (int r = threadIdx.x; r < row; r += blockDim.x) off += ent_n[r];
+  int total;
+  (void)block_excl_scan(off, part, &total);
+  off = total;
+  const int n = ent_n[row];
+  const double *src = ent + 7 * (size_t)row * C;
+  double *dst = list + 7 * (size_t)off;
+  for (int i = threadIdx.x; i < 7 * n; i += blockDim.x) dst[i] = src[i];
+  if (row == R - 1 && threadIdx.x == 0) {
+    count[0] = off + n;
+    double q = 0.0;
+    for (int r = 0; r < R; ++r) q += sums[6 * (size_t)r + 5];
+    count[1] = (int32_t)q;
+  }
 }
 
 // ============================================================ global mode
@@ -2003,18 +2134,27 @@ struct Pair3 {
 };
 // record cursors for knn_one: load() = packed coordinates of the current
 // pair of records, next() = the following pair
-struct LdsPairCursor {  // pair-interleaved LDS tile (x0 x1 y0 y1 z0 z1 i0 i1)
-  const float *p;
+// The k_knn LDS tile, pair-interleaved in two planes of 16 B per pair of
+// records: XY (x0 x1 y0 y1) and, kZgOff floats further, ZG (z0 z1 g0 g1).
+// A 16-B stride spreads the lanes' b128 reads over all bank quads (one 32-B
+// pair stride used only every other quad: a 2-way conflict floor).
+#ifndef NAVGPU_TILE_REC
+#define NAVGPU_TILE_REC 1600
+#endif
+constexpr int kTilePairs = NAVGPU_TILE_REC / 2 + 2;  // two spare pairs: read-ahead
+constexpr int kZgOff = 4 * kTilePairs;
+struct LdsPairCursor {
+  const float *p;  // XY plane, pair P at p = XY + 4 P
   __device__ Pair3 load() const {
     const float4 xy = *(const float4 *)p;
-    const float2 zz = *(const float2 *)(p + 4);
+    const float2 zz = *(const float2 *)(p + kZgOff);
     Pair3 P;
     P.x = f2{xy.x, xy.y};
     P.y = f2{xy.z, xy.w};
     P.z = f2{zz.x, zz.y};
     return P;
   }
-  __device__ void next() { p += 8; }
+  __device__ void next() { p += 4; }
 };
 struct RecPairCursor {  // global Rec16 array (two records of padding at its end)
   const Rec16 *p;
@@ -2300,9 +2440,6 @@ __device__ __forceinline__ void knn_one(
 #ifndef NAVGPU_TILE_THREADS
 #define NAVGPU_TILE_THREADS 192  // 3 waves: a ~150-query tile fills them
 #endif
-#ifndef NAVGPU_TILE_REC
-#define NAVGPU_TILE_REC 1600
-#endif
 constexpr int kTileThreads = NAVGPU_TILE_THREADS;
 constexpr int kTileRec = NAVGPU_TILE_REC;  // records staged per tile (16 B each)
 #ifndef NAVGPU_STAGE_U
@@ -2344,7 +2481,7 @@ __global__ __launch_bounds__(kTileThreads, NAVGPU_KNN_MINW) NAVGPU_KNN_ATTR void
   // g0 g1 (32 B; g = the record's cell-sorted position), so one b128 + one
   // b64 read gives packed operands; two spare pairs absorb the read-ahead
   // past a range's end
-  __shared__ __attribute__((aligned(16))) float spair[GLOBAL ? 8 : (kTileRec / 2 + 2) * 8];
+  __shared__ __attribute__((aligned(16))) float spair[GLOBAL ? 8 : 2 * kZgOff];
   // soff[r][i] = first record of cell xa - sx + i of row r; then, in place
   // (tile pass), cbase[r][j]: the LDS slot of the record at cell-sorted
   // position g of cell (row r, column j) is cbase[r][j] + g
@@ -2475,11 +2612,11 @@ __global__ __launch_bounds__(kTileThreads, NAVGPU_KNN_MINW) NAVGPU_KNN_ATTR void
             // so that a corrupt value cannot address outside the tile)
             const int jj = min(max(v[u].cx - xa + sx, 0), jmax);
             const int slot = soff[rr[u]][jj] + gg[u];
-            float *d = spair + (slot >> 1) * 8 + (slot & 1);
+            float *d = spair + (slot >> 1) * 4 + (slot & 1);
             d[0] = v[u].x;
             d[2] = v[u].y;
-            d[4] = v[u].z;
-            d[6] = __int_as_float(gg[u]);
+            d[kZgOff] = v[u].z;
+            d[kZgOff + 2] = __int_as_float(gg[u]);
           }
         }
       }
@@ -2507,8 +2644,8 @@ __global__ __launch_bounds__(kTileThreads, NAVGPU_KNN_MINW) NAVGPU_KNN_ATTR void
                         t0 = colst[i];
                         t1 = colst[i + 2 * sx + 1];
                       },
-                      [&](int t) { return LdsPairCursor{spair + (t >> 1) * 8}; },
-                      [&](int p) { return __float_as_int(spair[(p >> 1) * 8 + 6 + (p & 1)]); },
+                      [&](int t) { return LdsPairCursor{spair + (t >> 1) * 4}; },
+                      [&](int p) { return __float_as_int(spair[kZgOff + (p >> 1) * 4 + 2 + (p & 1)]); },
                       oidx, odist, L_);
       } else {
         knn_one<K, 9>(G, tsort, qv, c, q,
@@ -2804,7 +2941,7 @@ namespace {
 enum Slot {
   kBBox = 1, kParams, kCnt, kStart, kBSum, kCellId, kSlotBuf, kRec, kTan,
   kKdFc, kKdP, kKdT, kQStart, kQCell, kQSlot, kQPerm, kStats, kOvf, kSlowQ,
-  kSlowThr, kTSort, kRowMaskS, kRowMaskT, kRowTie,
+  kSlowThr, kTSort, kRowMaskS, kRowMaskT, kRowTie, kCorrEnt, kCorrN, kCorrSums,
   kH0 = 100, kH1, kH2, kH3, kH4, kH5,
 };
 
@@ -3276,12 +3413,46 @@ int navgpu_rows_corr_dev(navgpu_ctx *ctx, const double *tree_pts,
   ARG_CHECK(tree_pts && tree_n && nn_pos && nn_dist && ori && sums);
   int HS = 64;
   while (HS < 2 * C) HS <<= 1;
-  const int lds = HS * (8 + 4 + 4) + 4 * C;
+  const int lds = HS * (8 + 4 + 4 + 4) + 4 * C;
   RC(set_lds(k_rows_corr, lds));
   TimedRegion tr(ctx, "rows_corr");
   hipLaunchKernelGGL(k_rows_corr, dim3(R), dim3(kCorrBlock), lds, ctx->stream, tree_pts,
-                     tree_n, nn_pos, nn_dist, ori, C, HS, keep, sums);
+                     tree_n, nn_pos, nn_dist, ori, C, HS, keep, sums, nullptr, nullptr);
   CHECK_LAUNCH("k_rows_corr");
+  return NAVGPU_OK;
+}
+
+int navgpu_rows_corr_list_dev(navgpu_ctx *ctx, const double *tree_pts,
+                              const int32_t *tree_n, const int32_t *nn_pos,
+                              const double *nn_dist, const double *ori, int R, int C,
+                              double *list, int32_t *count) {
+  ARG_CHECK(ctx && R >= 0 && C >= 0);
+  if (C > kMaxRowCols) {
+    set_err("rows_corr_list: C=%d exceeds %d", C, kMaxRowCols);
+    return NAVGPU_ERANGE;
+  }
+  ARG_CHECK(count);
+  if ((size_t)R * C == 0) {
+    HIP_TRY(hipMemsetAsync(count, 0, 8, ctx->stream));
+    return NAVGPU_OK;
+  }
+  ARG_CHECK(tree_pts && tree_n && nn_pos && nn_dist && ori && list);
+  int HS = 64;
+  while (HS < 2 * C) HS <<= 1;
+  const int lds = HS * (8 + 4 + 4 + 4) + 4 * C;
+  double *ent, *sums;
+  int32_t *ent_n;
+  RC(ws(ctx, kCorrEnt, 7 * (size_t)R * C, &ent));
+  RC(ws(ctx, kCorrN, (size_t)R, &ent_n));
+  RC(ws(ctx, kCorrSums, 6 * (size_t)R, &sums));
+  RC(set_lds(k_rows_corr, lds));
+  TimedRegion tr(ctx, "rows_corr");
+  hipLaunchKernelGGL(k_rows_corr, dim3(R), dim3(kCorrBlock), lds, ctx->stream, tree_pts,
+                     tree_n, nn_pos, nn_dist, ori, C, HS, nullptr, sums, ent, ent_n);
+  CHECK_LAUNCH("k_rows_corr");
+  hipLaunchKernelGGL(k_corr_pack, dim3(R), dim3(256), 0, ctx->stream, ent, ent_n, sums, R, C,
+                     list, count);
+  CHECK_LAUNCH("k_corr_pack");
   return NAVGPU_OK;
 }
 
@@ -3438,9 +3609,33 @@ int navgpu_kd_build_dev(navgpu_ctx *ctx, double *pts, size_t n, int depth0) {
   RC(ws(ctx, kKdFc, 3 * n, &fc));
   RC(ws(ctx, kKdP, n, &P));
   RC(ws(ctx, kKdT, n, &T));
-  hipLaunchKernelGGL(k_kd_build_global, dim3(1), dim3(1024), 0, ctx->stream,
-                     pts, ni, depth0 % 3, fc, P, T);
-  CHECK_LAUNCH("k_kd_build_global");
+  // levels above the leaves: until every subarray (<= ceil(n / 2^L)) fits
+  // the LDS build of k_kd_leaves
+  int L = 0;
+  while (L < 30 && !(((n + ((size_t)1 << L) - 1) >> L) <= 65535 &&
+                     kd_build_lds_bytes((int)((n + ((size_t)1 << L) - 1) >> L)) <= lds_limit()))
+    ++L;
+  if (getenv("NAVGPU_KD_ONE_WG") || L >= 24) {  // the single-workgroup build (reference for tests)
+    hipLaunchKernelGGL(k_kd_build_global, dim3(1), dim3(1024), 0, ctx->stream,
+                       pts, ni, depth0 % 3, fc, P, T);
+    CHECK_LAUNCH("k_kd_build_global");
+    return NAVGPU_OK;
+  }
+  hipLaunchKernelGGL(k_kd_prep, dim3(grid1d(n, 256)), dim3(256), 0, ctx->stream, pts, ni, fc, P);
+  CHECK_LAUNCH("k_kd_prep");
+  for (int d = 0; d < L; ++d) {
+    hipLaunchKernelGGL(k_kd_level, dim3(1u << d), dim3(1024), 0, ctx->stream, fc, ni,
+                       depth0 % 3, d, P, T);
+    CHECK_LAUNCH("k_kd_level");
+  }
+  hipLaunchKernelGGL(k_kd_gather, dim3(grid1d(n, 256)), dim3(256), 0, ctx->stream, pts, fc, ni, P);
+  CHECK_LAUNCH("k_kd_gather");
+  const int leaf = (int)((n + ((size_t)1 << L) - 1) >> L);
+  const int lds = kd_build_lds_bytes(leaf);
+  RC(set_lds(k_kd_leaves, lds));
+  hipLaunchKernelGGL(k_kd_leaves, dim3(1u << L), dim3(1024), lds, ctx->stream, pts, fc, ni,
+                     depth0 % 3, L, P);
+  CHECK_LAUNCH("k_kd_leaves");
   return NAVGPU_OK;
 }
 

@@ -258,28 +258,17 @@ int navslam_last_frame_stats(int *queries, int *correspondences, int *iterations
 }
 
 /* ------------------------------------------------ SLAM_attr side table */
-/* dedup hash slot: a nearest point's coordinates -> its correspondence */
-typedef struct {
-    double key[3];
-    int32_t idx;
-} dedup_slot;
 
 typedef struct {
     SLAM_attr *key;
-    double *d_lidar, *d_global, *d_last, *d_tree, *d_dist, *d_sums;
+    double *d_lidar, *d_global, *d_last, *d_tree, *d_dist, *d_sums, *d_list;
     double h_sums[6 * ROWS];
-    int32_t *d_tcol, *d_tn, *d_pos;
+    int32_t *d_tcol, *d_tn, *d_pos, *d_count;
     int have_trees;
     double h_tree[NPTS * 3];
     int32_t h_tn[ROWS];
     KDNode *roots[ROWS];
-    /* localisation scratch */
-    double h_tp[NPTS * 3];
-    double h_dist[NPTS];
-    int32_t h_pos[NPTS];
     NeighborResult *result; /* correspondence list (src/slam.c:214) */
-    dedup_slot *tab;
-    int32_t *used;
 } slam_state;
 
 static slam_state **g_states;
@@ -306,6 +295,8 @@ static slam_state *state_for(SLAM_attr *a)
     CK(navgpu_malloc(c, 4 * ROWS, (void **)&s->d_tn));
     CK(navgpu_malloc(c, 4 * NPTS, (void **)&s->d_pos));
     CK(navgpu_malloc(c, 8 * 6 * ROWS, (void **)&s->d_sums));
+    CK(navgpu_malloc(c, 56 * (size_t)NPTS, (void **)&s->d_list));
+    CK(navgpu_malloc(c, 8, (void **)&s->d_count));
     g_states = realloc(g_states, sizeof(*g_states) * (g_nstates + 1));
     g_states[g_nstates++] = s;
     return s;
@@ -377,23 +368,6 @@ void slam_mapping(SLAM_attr *attr, Pos pos, PointCloud *lidarPointCloud)
     attr->frameCount++;
 }
 
-
-static uint64_t key_bits(double v)
-{
-    if (v == 0.0)
-        v = 0.0; /* -0.0 == 0.0 in the reference's comparison */
-    uint64_t b;
-    memcpy(&b, &v, 8);
-    return b;
-}
-
-static uint64_t hash3(const double *p)
-{
-    uint64_t h = key_bits(p[0]) * 0x9E3779B97F4A7C15ull;
-    h ^= key_bits(p[1]) + 0x632BE59BD9B4E019ull + (h << 6) + (h >> 2);
-    h ^= key_bits(p[2]) + 0x85EBCA77C2B2AE63ull + (h << 6) + (h >> 2);
-    return h ^ (h >> 29);
-}
 
 /* The NAVSLAM_ADAM=fast tail of slam_localization: dedup + residual sums on
  * the GPU (navgpu_rows_corr_dev), then src/slam.c:300-389's Adam loop with
@@ -513,80 +487,28 @@ Pos slam_localization(SLAM_attr *attr, PointCloud *lidarPointCloud,
                                 ROWS, COLS, s->d_pos, s->d_dist, NULL));
     if (adam_fast())
         return localization_fast(attr, s, transform, pos_last);
-    CK(navgpu_download(c, s->h_pos, s->d_pos, 4 * NPTS));
-    CK(navgpu_download(c, s->h_dist, s->d_dist, 8 * NPTS));
-    CK(navgpu_download(c, s->h_tp, s->d_global, 24 * NPTS));
-    CK(navgpu_sync(c));
-
-    /* host: dedup (src/slam.c:235-284) */
-    /* per-state scratch, allocated once (a fresh 56 B x R*C list every frame
-     * costs its page faults again) */
-    size_t tcap = 16;
-    while (tcap < 2 * (size_t)COLS)
-        tcap <<= 1;
+    /* GPU: the reference's correspondence list (src/slam.c:235-284), built
+     * and compacted in its first-insertion order on the device; only the
+     * list itself comes back */
     if (!s->result) {
         s->result = malloc(sizeof(NeighborResult) * (NPTS ? NPTS : 1));
-        s->tab = malloc(sizeof(dedup_slot) * tcap);
-        s->used = malloc(sizeof(int32_t) * tcap);
-        if (!s->result || !s->tab || !s->used) {
+        if (!s->result) {
             fprintf(stderr, "navslam: out of host memory\n");
             abort();
         }
     }
+    _Static_assert(sizeof(NeighborResult) == 7 * sizeof(double),
+                   "NeighborResult is 7 doubles (utils/kdtree.h:14-18)");
+    CK(navgpu_rows_corr_list_dev(c, s->d_tree, s->d_tn, s->d_pos, s->d_dist, s->d_global,
+                                 ROWS, COLS, s->d_list, s->d_count));
+    int32_t cnt[2];
+    CK(navgpu_download(c, cnt, s->d_count, sizeof(cnt)));
+    CK(navgpu_sync(c));
+    int CPcount = cnt[0], nqueries = cnt[1];
     NeighborResult *result = s->result;
-    dedup_slot *tab = s->tab;
-    int32_t *used = s->used;
-    for (size_t i = 0; i < tcap; i++)
-        tab[i].idx = -1;
-    int CPcount = 0, nqueries = 0;
-    for (int row = 0; row < ROWS; ++row) {
-        int nused = 0;
-        const double *tree = s->h_tree + 3 * (size_t)row * COLS;
-        for (int col = 0; col < COLS; ++col) {
-            size_t g = (size_t)row * COLS + col;
-            int32_t pos = s->h_pos[g];
-            /* non-feature cells, and features of an empty row tree (where the
-             * reference reads an uninitialised Point, src/slam.c:242-252):
-             * no correspondence */
-            if (pos < 0)
-                continue;
-            nqueries++;
-            const double *np = tree + 3 * (size_t)pos;
-            double bestDist = s->h_dist[g];
-            int nan = np[0] != np[0] || np[1] != np[1] || np[2] != np[2];
-            size_t h = nan ? 0 : (size_t)(hash3(np) & (tcap - 1));
-            int found = -1;
-            if (!nan) {
-                while (tab[h].idx >= 0) {
-                    const double *k = tab[h].key;
-                    if (k[0] == np[0] && k[1] == np[1] && k[2] == np[2]) {
-                        found = tab[h].idx;
-                        break;
-                    }
-                    h = (h + 1) & (tcap - 1);
-                }
-            }
-            if (found >= 0) {
-                if (result[found].distance > bestDist) {
-                    memcpy(&result[found].oriPoint, s->h_tp + 3 * g, 24);
-                    memcpy(&result[found].nearestPoint, np, 24);
-                    result[found].distance = bestDist;
-                }
-                continue;
-            }
-            memcpy(&result[CPcount].oriPoint, s->h_tp + 3 * g, 24);
-            memcpy(&result[CPcount].nearestPoint, np, 24);
-            result[CPcount].distance = bestDist;
-            if (!nan) {
-                memcpy(tab[h].key, np, 24);
-                tab[h].idx = CPcount;
-                used[nused++] = (int32_t)h;
-            }
-            CPcount++;
-        }
-        for (int i = 0; i < nused; i++)
-            tab[used[i]].idx = -1;
-    }
+    if (CPcount > 0)
+        CK(navgpu_download(c, result, s->d_list, sizeof(NeighborResult) * (size_t)CPcount));
+    CK(navgpu_sync(c));
 
     /* host: Adam on the translation (src/slam.c:218-379) */
     double learningRate = 0.1, tolerance = 1e-6;

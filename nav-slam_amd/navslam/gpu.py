@@ -46,6 +46,8 @@ def _declare(L):
                                                C.c_int, _vp, _vp, _vp]),
         "navgpu_rows_corr_dev": (C.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, C.c_int,
                                            C.c_int, _vp, _vp]),
+        "navgpu_rows_corr_list_dev": (C.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, C.c_int,
+                                               C.c_int, _vp, _vp]),
         "navgpu_rows_match_dev": (C.c_int, [_vp, _vp, _vp, C.c_int, C.c_int,
                                             _vp, _vp, _vp, _vp]),
         "navgpu_rows_match_host": (C.c_int, [_vp, _vp, _vp, C.c_int, C.c_int,
@@ -234,6 +236,9 @@ class NavGpu:
                                                 _ptr(tr), _ptr(out), _ptr(out_last)),
                     "transform_dev")
 
+    def kd_build_dev(self, pts, n, depth0=0):
+        self._check(self.L.navgpu_kd_build_dev(self.h, _ptr(pts), n, depth0), "kd_build_dev")
+
     def kd_build_rows_dev(self, feat_src, coords, R, Cc, tree_pts, tree_col, tree_n,
                           mask=None):
         self._check(self.L.navgpu_kd_build_rows_dev(
@@ -250,6 +255,11 @@ class NavGpu:
         self._check(self.L.navgpu_rows_corr_dev(
             self.h, _ptr(tree_pts), _ptr(tree_n), _ptr(nn_pos), _ptr(nn_dist), _ptr(ori),
             R, Cc, _ptr(keep), _ptr(sums)), "rows_corr")
+
+    def rows_corr_list_dev(self, tree_pts, tree_n, nn_pos, nn_dist, ori, R, Cc, lst, count):
+        self._check(self.L.navgpu_rows_corr_list_dev(
+            self.h, _ptr(tree_pts), _ptr(tree_n), _ptr(nn_pos), _ptr(nn_dist), _ptr(ori), R, Cc,
+            _ptr(lst), _ptr(count)), "rows_corr_list_dev")
 
     def rows_match_dev(self, src, tgt, R, Cc, src_mask, tgt_mask, nn_idx, nn_dist):
         self._check(self.L.navgpu_rows_match_dev(

@@ -96,6 +96,31 @@ def test_kd_build_large_and_depth_offset(gpu, orc, n, depth0):
     del ix
 
 
+@pytest.mark.parametrize("n,depth0,integer", [(1_000_000, 0, False), (1_000_000, 2, True),
+                                              (300_001, 1, False)])
+def test_kd_build_million_level_parallel(gpu, orc, n, depth0, integer):
+    """buildKDTree (utils/kdtree.c:20-82) beyond one workgroup's LDS: the
+    level-parallel build (a workgroup per subarray per level, then one per
+    LDS-sized subtree) gives the reference permutation, also with heavy
+    duplicates and a shifted root axis."""
+    rng = np.random.default_rng(n + depth0)
+    pts = rng.uniform(-5000, 5000, (n, 3))
+    if integer:
+        pts = np.round(pts / 50.0)
+    rot = np.roll(pts, -depth0, axis=1)
+    t, _ = orc.kd_build(rot)
+    _eq(gpu.kd_build(pts, depth0), np.roll(t, depth0, axis=1), f"n={n} depth0={depth0}")
+
+
+def test_kd_build_level_parallel_equals_single_workgroup(gpu, monkeypatch):
+    rng = np.random.default_rng(9)
+    pts = np.round(rng.uniform(0, 300, (40000, 3)))
+    a = gpu.kd_build(pts, 1)
+    monkeypatch.setenv("NAVGPU_KD_ONE_WG", "1")
+    b = gpu.kd_build(pts, 1)
+    _eq(a, b, "level-parallel vs single-workgroup build")
+
+
 # ------------------------------------------------------ R4-R6 per-row mode
 def test_rows_match_l9_golden(gpu, golden):
     g = golden("rows_l9")
@@ -586,6 +611,44 @@ def test_rows_corr_matches_reference_dedup(gpu, orc, integer_mm):
     _eq(keep.cpu().numpy(), ek, "kept correspondences")
     np.testing.assert_allclose(sums.cpu().numpy(), es, rtol=1e-12, atol=1e-9)
     assert ek.sum() > 0 and (ek.sum() < (pos.cpu().numpy() >= 0).sum() or not integer_mm)
+
+
+@pytest.mark.parametrize("integer_mm", [False, True])
+def test_rows_corr_list_matches_reference_list(gpu, orc, integer_mm):
+    """The exact mode's correspondence list built on the GPU
+    (navgpu_rows_corr_list_dev) == the reference list (src/slam.c:235-284
+    through orc_rows_dedup, pinned by the slam8x8 golden): same entries in
+    the same order, bit for bit (oriPoint, nearestPoint, distance)."""
+    import torch
+    from navslam.synth import l9_pair
+    src, tgt = l9_pair(24, 640, seed=23, integer_mm=integer_mm)
+    src[3, 100:110] = np.nan  # NaN queries: no nearest point, no entry
+    tgt[5, 50:60, 1] = np.nan  # NaN tree points: entries of their own
+    R, Cc = src.shape[:2]
+    dev = torch.device("cuda", 0)
+    ss, ts = torch.from_numpy(src).to(dev), torch.from_numpy(tgt).to(dev)
+    tree = torch.empty_like(ts)
+    tcol = torch.empty((R, Cc), dtype=torch.int32, device=dev)
+    tn = torch.empty(R, dtype=torch.int32, device=dev)
+    pos = torch.empty((R, Cc), dtype=torch.int32, device=dev)
+    dist = torch.empty((R, Cc), dtype=torch.float64, device=dev)
+    lst = torch.full((R * Cc, 7), -7.0, dtype=torch.float64, device=dev)
+    cnt = torch.zeros(2, dtype=torch.int32, device=dev)
+    ori = ss + 0.25  # transformed frame (the oriPoint source)
+    torch.cuda.synchronize()
+    gpu.kd_build_rows_dev(ts, ts, R, Cc, tree, tcol, tn)
+    gpu.kd_query_rows_dev(tree, tn, ss, ss, R, Cc, pos, dist)
+    gpu.rows_corr_list_dev(tree, tn, pos, dist, ori, R, Cc, lst, cnt)
+    gpu.sync()
+    o, nr, d, _ = orc.rows_dedup(tree.cpu().numpy(), pos.cpu().numpy().astype(np.int64),
+                                 dist.cpu().numpy(), ori.cpu().numpy())
+    n, nq = (int(v) for v in cnt.cpu().numpy())
+    assert n == len(d) and n > 0
+    assert nq == int((pos.cpu().numpy() >= 0).sum())
+    got = lst.cpu().numpy()[:n]
+    _eq(got[:, 0:3], o, "oriPoint")
+    _eq(got[:, 3:6], nr, "nearestPoint")
+    _eq(got[:, 6], d, "distance")
 
 
 @pytest.mark.parametrize("R,Cc,F,steps", [(54, 42, 4, 9), (128, 2048, 3, 4)])
