@@ -1334,6 +1334,247 @@ __global__ __launch_bounds__(256) void k_kd_prep(const double *__restrict__ pts,
   P[i] = (uint32_t)i;
 }
 
+// ---- Grid-wide Lomuto passes for the top levels of a large build.
+// One pass of the reference nth_element (utils/kdtree.c:20-52) over a window
+// [first, last] (pivot = P[last], m = last - first positions before it) is
+// a stable compaction of the smalls plus the "tape" of the larges: with
+// c(p) = smalls before p, tape[p] = elem(p) for a large p and tape[c(p)]
+// for a small one; the window becomes smalls | pivot | tape[S+1..m) and
+// tape[S] moves to last (the same rule wave_nth_element resolves within a
+// wave). Here every window of a level runs at once, each over many
+// workgroups: k_sel_count (smalls per chunk), k_sel_rank (ranks from the
+// chunk prefix, smalls compacted into Ptmp, tape words into W: bit 31 =
+// resolved element, else the position it copies), k_sel_jump (tape chains
+// followed kSelHops hops per round, in place: a chain of length M resolves in
+// log_kSelHops(M) rounds; a round starts only if the last left work),
+// k_sel_scatter (the new window contents), k_sel_update (quickselect's next
+// window: i = first + S; done at nth).
+constexpr int kSelThreads = 256, kSelPer = 16, kSelChunk = kSelThreads * kSelPer;
+constexpr int kSelHops = 64;
+constexpr int kSelFinishMax = 8192;  // windows this short finish in one workgroup's LDS
+constexpr uint32_t kSelRes = 0x80000000u;
+
+struct SelState {
+  int *first, *last, *nth, *act, *S, *pivot, *cnt;  // per window (cnt: [nW][nb])
+  int *unres;                                       // per jump round
+  int *nact;                                        // active windows after update
+  int nb, nW;
+};
+
+__global__ __launch_bounds__(256) void k_sel_init(SelState st, int n, int d) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= st.nW) return;
+  int lo, hi;
+  kd_node_range(n, d, k, lo, hi);
+  st.first[k] = lo;
+  st.last[k] = hi - 1;
+  st.nth[k] = lo + (hi - lo) / 2;
+  st.act[k] = hi - lo < 2 ? 0 : (hi - lo <= kSelFinishMax ? 2 : 1);
+}
+
+__global__ __launch_bounds__(kSelThreads) void k_sel_count(SelState st,
+                                                           const double *__restrict__ key,
+                                                           const uint32_t *__restrict__ P) {
+  __shared__ int red[kSelThreads / kWave];
+  const int k = blockIdx.y, b = blockIdx.x;
+  if (st.act[k] != 1) return;
+  const int first = st.first[k], last = st.last[k], m = last - first;
+  const int p0 = b * kSelChunk;
+  if (p0 >= m) return;
+  const uint32_t pe = P[last];
+  const double pk = key[pe];
+  int c = 0;
+#pragma unroll 4
+  for (int i = 0; i < kSelPer; ++i) {
+    const int p = p0 + i * kSelThreads + (int)threadIdx.x;
+    if (p < m) c += (key[P[first + p]] - pk) <= 0.0;  // kdtree.c:31-43
+  }
+  for (int o = kWave / 2; o > 0; o >>= 1) c += __shfl_xor(c, o, kWave);
+  if ((threadIdx.x & (kWave - 1)) == 0) red[threadIdx.x / kWave] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int t = 0;
+    for (int w = 0; w < kSelThreads / kWave; ++w) t += red[w];
+    st.cnt[k * st.nb + b] = t;
+    if (b == 0) st.pivot[k] = (int)pe;
+  }
+}
+
+__global__ __launch_bounds__(kSelThreads) void k_sel_rank(SelState st,
+                                                          const double *__restrict__ key,
+                                                          const uint32_t *__restrict__ P,
+                                                          uint32_t *__restrict__ Ptmp,
+                                                          uint32_t *__restrict__ W) {
+  __shared__ int wc[kSelThreads / kWave + 1];
+  __shared__ int sbefore, stotal;
+  const int k = blockIdx.y, b = blockIdx.x;
+  if (st.act[k] != 1) return;
+  const int first = st.first[k], last = st.last[k], m = last - first;
+  const int p0 = b * kSelChunk;
+  if (p0 >= m) return;
+  const int nbk = (m + kSelChunk - 1) / kSelChunk;
+  const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
+  if (wid == 0) {  // smalls before this chunk, and the window's total
+    int bef = 0, tot = 0;
+    for (int j = lane; j < nbk; j += kWave) {
+      const int c = st.cnt[k * st.nb + j];
+      tot += c;
+      bef += j < b ? c : 0;
+    }
+    for (int o = kWave / 2; o > 0; o >>= 1) {
+      bef += __shfl_xor(bef, o, kWave);
+      tot += __shfl_xor(tot, o, kWave);
+    }
+    if (lane == 0) {
+      sbefore = bef;
+      stotal = tot;
+    }
+  }
+  const double pk = key[P[last]];
+  __syncthreads();
+  int base = sbefore;
+  if (b == 0 && threadIdx.x == 0) st.S[k] = stotal;
+  for (int i = 0; i < kSelPer; ++i) {
+    const int p = p0 + i * kSelThreads + (int)threadIdx.x;
+    const bool in = p < m;
+    const uint32_t e = in ? P[first + p] : 0u;
+    const bool small = in && (key[e] - pk) <= 0.0;
+    const unsigned long long bal = __ballot(small);
+    if (lane == 0) wc[wid] = __popcll(bal);
+    __syncthreads();
+    int before = base, tot = 0;
+    for (int w = 0; w < kSelThreads / kWave; ++w) {
+      before += w < wid ? wc[w] : 0;
+      tot += wc[w];
+    }
+    const int sp = before + lanes_below(bal);
+    if (small) Ptmp[first + sp] = e;
+    if (in) W[first + p] = (small && sp != p) ? (uint32_t)sp : (kSelRes | e);
+    base += tot;
+    __syncthreads();
+  }
+}
+
+// The tape values the window needs are those of [S, m): one position per
+// thread follows its chain up to kSelHops hops and stores how far it got.
+__global__ __launch_bounds__(kSelThreads) void k_sel_jump0(SelState st, uint32_t *W) {
+  const int k = blockIdx.y;
+  if (st.act[k] != 1) return;
+  const int first = st.first[k], m = st.last[k] - first;
+  const int q = st.S[k] + (int)(blockIdx.x * kSelThreads + threadIdx.x);
+  int left = 0;
+  if (q < m) {
+    uint32_t w = W[first + q];
+    if (!(w & kSelRes)) {
+      for (int h = 0; h < kSelHops && !(w & kSelRes); ++h) w = W[first + (int)w];
+      W[first + q] = w;
+      left = !(w & kSelRes);
+    }
+  }
+  left = __syncthreads_count(left);
+  if (threadIdx.x == 0 && left) atomicAdd(&st.unres[0], left);
+}
+
+// Chains k_sel_jump0 left unresolved (long ones only): every position of the
+// window jumps kSelHops hops in place, shortening all chains that many
+// times; runs only when round - 1 left work.
+__global__ __launch_bounds__(kSelThreads) void k_sel_jump(SelState st, uint32_t *W, int round) {
+  const int k = blockIdx.y, b = blockIdx.x;
+  if (st.act[k] != 1 || (round > 0 && st.unres[round - 1] == 0)) return;
+  const int first = st.first[k], m = st.last[k] - first;
+  const int p0 = b * kSelChunk;
+  if (p0 >= m) return;
+  int left = 0;
+  for (int i = 0; i < kSelPer; ++i) {
+    const int p = p0 + i * kSelThreads + (int)threadIdx.x;
+    if (p >= m) break;
+    uint32_t w = W[first + p];
+    if (w & kSelRes) continue;
+    for (int h = 0; h < kSelHops && !(w & kSelRes); ++h) w = W[first + (int)w];
+    W[first + p] = w;
+    left += !(w & kSelRes);
+  }
+  left = __syncthreads_count(left > 0);
+  if (threadIdx.x == 0 && left) atomicAdd(&st.unres[round], left);
+}
+
+__global__ __launch_bounds__(kSelThreads) void k_sel_scatter(SelState st,
+                                                             uint32_t *__restrict__ P,
+                                                             const uint32_t *__restrict__ Ptmp,
+                                                             const uint32_t *__restrict__ W) {
+  const int k = blockIdx.y, b = blockIdx.x;
+  if (st.act[k] != 1) return;
+  const int first = st.first[k], last = st.last[k], m = last - first;
+  const int p0 = b * kSelChunk;
+  if (p0 >= m) return;
+  const int S = st.S[k];  // S == m: no tape, the pivot stays at last
+  // a chain the jump rounds left unresolved (only past both rounds' 64^2
+  // hops): followed to its end here; W is read-only in this kernel
+  auto tape = [&](int q) {
+    uint32_t w = W[first + q];
+    while (!(w & kSelRes)) w = W[first + (int)w];
+    return w & ~kSelRes;
+  };
+  for (int i = 0; i < kSelPer; ++i) {
+    const int p = p0 + i * kSelThreads + (int)threadIdx.x;
+    if (p >= m) break;
+    if (p < S)
+      P[first + p] = Ptmp[first + p];
+    else if (p == S) {
+      P[first + S] = (uint32_t)st.pivot[k];
+      if (S < m) P[last] = tape(S);
+    } else
+      P[first + p] = tape(p);
+  }
+}
+
+__global__ __launch_bounds__(256) void k_sel_update(SelState st, int rounds) {
+  __shared__ int cnt;
+  if (threadIdx.x == 0) cnt = 0;
+  __syncthreads();
+  for (int k = threadIdx.x; k < st.nW; k += blockDim.x) {
+    if (st.act[k] != 1) continue;
+    const int i = st.first[k] + st.S[k], nth = st.nth[k];
+    int a = 1;
+    if (i == nth)
+      a = 0;
+    else if (i < nth)
+      st.first[k] = i + 1;
+    else
+      st.last[k] = i - 1;
+    if (st.first[k] >= st.last[k]) a = 0;
+    if (a && st.last[k] - st.first[k] + 1 <= kSelFinishMax) a = 2;
+    st.act[k] = a;
+    if (a == 1) atomicAdd(&cnt, 1);
+  }
+  if (threadIdx.x < rounds) st.unres[threadIdx.x] = 0;
+  __syncthreads();
+  if (threadIdx.x == 0) *st.nact = cnt;
+}
+
+// The rest of a window's nth_element once it holds <= kSelFinishMax
+// positions: the window's ids and keys in LDS, block_nth_element there
+// (local indices), the permuted ids written back.
+__global__ __launch_bounds__(1024) void k_sel_finish(SelState st, const double *__restrict__ key,
+                                                     uint32_t *__restrict__ P) {
+  const int k = blockIdx.x;
+  if (st.act[k] != 2) return;
+  const int first = st.first[k], m = st.last[k] - first + 1;
+  double *kl = (double *)smem;
+  uint32_t *gid = (uint32_t *)(smem + 8 * kSelFinishMax);
+  uint16_t *pl = (uint16_t *)(gid + kSelFinishMax);
+  uint16_t *tl = pl + kSelFinishMax;
+  for (int i = threadIdx.x; i < m; i += blockDim.x) {
+    const uint32_t e = P[first + i];
+    gid[i] = e;
+    kl[i] = key[e];
+    pl[i] = (uint16_t)i;
+  }
+  __syncthreads();
+  block_nth_element<uint16_t>(kl, pl, tl, 0, m - 1, st.nth[k] - first);
+  for (int i = threadIdx.x; i < m; i += blockDim.x) P[first + i] = gid[pl[i]];
+}
+
 // pts[i] = point P[i]: places the upper levels' nodes (the leaves kernel
 // then overwrites every leaf subarray with its built subtree)
 __global__ __launch_bounds__(256) void k_kd_gather(double *__restrict__ pts,
@@ -2941,7 +3182,7 @@ namespace {
 enum Slot {
   kBBox = 1, kParams, kCnt, kStart, kBSum, kCellId, kSlotBuf, kRec, kTan,
   kKdFc, kKdP, kKdT, kQStart, kQCell, kQSlot, kQPerm, kStats, kOvf, kSlowQ,
-  kSlowThr, kTSort, kRowMaskS, kRowMaskT, kRowTie, kCorrEnt, kCorrN, kCorrSums,
+  kSlowThr, kTSort, kRowMaskS, kRowMaskT, kRowTie, kCorrEnt, kCorrN, kCorrSums, kKdPtmp, kKdSel,
   kH0 = 100, kH1, kH2, kH3, kH4, kH5,
 };
 
@@ -3623,10 +3864,75 @@ int navgpu_kd_build_dev(navgpu_ctx *ctx, double *pts, size_t n, int depth0) {
   }
   hipLaunchKernelGGL(k_kd_prep, dim3(grid1d(n, 256)), dim3(256), 0, ctx->stream, pts, ni, fc, P);
   CHECK_LAUNCH("k_kd_prep");
+  // levels whose subarrays exceed kSelMinLen: grid-wide passes over all of
+  // a level's windows at once; below: a workgroup per subarray
+  constexpr int kSelMinLen = 0;  // NAVGPU_KD_NO_SEL=1: a workgroup per subarray at every level
+  uint32_t *Ptmp;
+  RC(ws(ctx, kKdPtmp, n, &Ptmp));
+  const int kRounds = 2;  // 64 hops, then 64 more of the compressed chains;
+                          // scatter follows whatever is left
+  int32_t *stbuf;
+  const int nWmax = 1 << std::max(0, L - 1);
+  const int nbmax = (int)((n + kSelChunk - 1) / kSelChunk);
+  RC(ws(ctx, kKdSel, (size_t)7 * nWmax + (size_t)nWmax * nbmax + kRounds + 1, &stbuf));
   for (int d = 0; d < L; ++d) {
-    hipLaunchKernelGGL(k_kd_level, dim3(1u << d), dim3(1024), 0, ctx->stream, fc, ni,
-                       depth0 % 3, d, P, T);
-    CHECK_LAUNCH("k_kd_level");
+    const int nW = 1 << d;
+    const int maxlen = (int)(n >> d);
+    if (maxlen < kSelMinLen || getenv("NAVGPU_KD_NO_SEL")) {
+      hipLaunchKernelGGL(k_kd_level, dim3(nW), dim3(1024), 0, ctx->stream, fc, ni,
+                         depth0 % 3, d, P, T);
+      CHECK_LAUNCH("k_kd_level");
+      continue;
+    }
+    SelState st;
+    st.nW = nW;
+    st.nb = (maxlen + kSelChunk - 1) / kSelChunk;
+    int32_t *q = stbuf;
+    st.first = q; q += nW;
+    st.last = q; q += nW;
+    st.nth = q; q += nW;
+    st.act = q; q += nW;
+    st.S = q; q += nW;
+    st.pivot = q; q += nW;
+    st.nact = q; q += nW;
+    st.unres = q; q += kRounds + 1;
+    st.cnt = q;
+    const double *key = fc + (size_t)((depth0 % 3 + d) % 3) * n;
+    hipLaunchKernelGGL(k_sel_init, dim3((nW + 255) / 256), dim3(256), 0, ctx->stream, st, ni, d);
+    CHECK_LAUNCH("k_sel_init");
+    HIP_TRY(hipMemsetAsync(st.unres, 0, 4 * (kRounds + 1), ctx->stream));
+    const dim3 grid(st.nb, nW);
+    // quickselect iterations until every window found its median; the
+    // active count is read back every few iterations
+    for (int it = 0; maxlen > kSelFinishMax; ++it) {
+      hipLaunchKernelGGL(k_sel_count, grid, dim3(kSelThreads), 0, ctx->stream, st, key, P);
+      hipLaunchKernelGGL(k_sel_rank, grid, dim3(kSelThreads), 0, ctx->stream, st, key, P, Ptmp,
+                         T);
+      hipLaunchKernelGGL(k_sel_jump0, dim3(st.nb * kSelPer, nW), dim3(kSelThreads), 0,
+                         ctx->stream, st, T);
+      for (int r = 1; r < kRounds; ++r)  // only if the round before left chains
+        hipLaunchKernelGGL(k_sel_jump, grid, dim3(kSelThreads), 0, ctx->stream, st, T, r);
+      hipLaunchKernelGGL(k_sel_scatter, grid, dim3(kSelThreads), 0, ctx->stream, st, P, Ptmp, T);
+      hipLaunchKernelGGL(k_sel_update, dim3(1), dim3(256), 0, ctx->stream, st, kRounds);
+      CHECK_LAUNCH("k_sel");
+      if (it > 4 * ni + 64) {  // quickselect shrinks its window every iteration
+        set_err("kd_build: selection did not converge (level %d)", d);
+        return NAVGPU_EHIP;
+      }
+      if (it % 4 == 3) {
+        int32_t nact = 0;
+        HIP_TRY(hipMemcpyAsync(&nact, st.nact, 4, hipMemcpyDeviceToHost, ctx->stream));
+        HIP_TRY(hipStreamSynchronize(ctx->stream));
+        if (getenv("NAVGPU_KD_TRACE"))
+          fprintf(stderr, "kd_build level %d (%d windows, %d max): it %d active %d\n", d, nW,
+                  maxlen, it, nact);
+        if (nact == 0) break;
+      }
+    }
+    const int flds = kSelFinishMax * (8 + 4 + 2 + 2);
+    RC(set_lds(k_sel_finish, flds));
+    hipLaunchKernelGGL(k_sel_finish, dim3(nW), dim3(1024), flds, ctx->stream, st, key, P);
+    CHECK_LAUNCH("k_sel_finish");
   }
   hipLaunchKernelGGL(k_kd_gather, dim3(grid1d(n, 256)), dim3(256), 0, ctx->stream, pts, fc, ni, P);
   CHECK_LAUNCH("k_kd_gather");

@@ -17,7 +17,7 @@ from navslam.gpu import NavGpu  # noqa: E402
 from pyoracle import Oracle  # noqa: E402
 
 dev = torch.device("cuda", 0)
-g = NavGpu(0, torch.cuda.current_stream(dev).cuda_stream)
+g = NavGpu(0)
 g.timing(True)
 out = {}
 for n in (1 << 20, 1 << 17):
@@ -31,10 +31,11 @@ for n in (1 << 20, 1 << 17):
         reps = 5
         for r in range(reps + 1):
             buf.copy_(src)
+            torch.cuda.synchronize()  # the library runs on its own stream
             if r == 1:
-                torch.cuda.synchronize()
                 g.timing_read("kd_build")
             g.kd_build_dev(buf, n, 0)
+            g.sync()
         torch.cuda.synchronize()
         ms, k = g.timing_read("kd_build")
         out[f"n{n}_{mode}_ms"] = round(ms / k, 3)
