@@ -1291,7 +1291,15 @@ __global__ __launch_bounds__(1024) void k_kd_build_lds(double *__restrict__ pts,
     FC[a * n + e] = pts[i];
   }
   __syncthreads();
+  // without the block-level loop below the root: on arbitrary point sets it
+  // costs more than it saves (n = 3000 / 5000: 306 / 546 us with it, 211 /
+  // 303 us without, scripts/kd_lds_time.py); it pays on scan rows only
+  // (k_rows_build)
+#ifdef NAVGPU_KD_LDS_LEVELS  // timing variant: with the loop
   block_build_kdtree<uint16_t>(FC, n, n, P, T, depth0);
+#else
+  block_build_kdtree<uint16_t, false, false>(FC, n, n, P, T, depth0);
+#endif
   for (int i = threadIdx.x; i < 3 * n; i += blockDim.x) {
     const int pos = i / 3, a = i % 3;
     pts[i] = FC[a * n + P[pos]];
@@ -1618,7 +1626,7 @@ __global__ __launch_bounds__(1024) void k_kd_leaves(double *__restrict__ pts,
     lf[2 * m + i] = FC[2 * (size_t)n + e];
   }
   __syncthreads();
-  block_build_kdtree<uint16_t>(lf, m, m, Pl, Tl, (depth0 + L) % 3);
+  block_build_kdtree<uint16_t, false, false>(lf, m, m, Pl, Tl, (depth0 + L) % 3);  // as k_kd_build_lds
   for (int i = threadIdx.x; i < 3 * m; i += blockDim.x) {
     const int pos = i / 3, a = i % 3;
     pts[3 * (size_t)lo + i] = lf[a * m + Pl[pos]];
@@ -1841,7 +1849,10 @@ struct GridParams {
 };
 
 // soff entries per staged row of a k_knn tile (W + 2 sx + 1 <= kTileCols)
-constexpr int kTileCols = 136;
+#ifndef NAVGPU_TILE_COLS
+#define NAVGPU_TILE_COLS 136
+#endif
+constexpr int kTileCols = NAVGPU_TILE_COLS;
 constexpr int kMaxSx = 8;
 #ifndef NAVGPU_KNN_SX
 #define NAVGPU_KNN_SX 1  // sx = 2: query stage 183 -> 177 us, build 99 -> 109 us (K3)
@@ -2756,31 +2767,24 @@ __global__ __launch_bounds__(kTileThreads, NAVGPU_KNN_MINW) NAVGPU_KNN_ATTR void
 #endif
     // staging is latency-bound: every thread issues all its global loads
     // before it writes any of them to LDS
-    {
-      constexpr int U = 4;  // soff entries per thread per batch
-      const int nsoff = 9 * ncell;
-      for (int e0 = 0; e0 < nsoff; e0 += U * (int)blockDim.x) {
-        int v[U];
+    // soff: the 9 rows (uniform loop, no index division), all loads first
+    for (int i0 = 0; i0 < ncell; i0 += (int)blockDim.x) {
+      const int i = i0 + (int)threadIdx.x;
+      int v[9];
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-          const int e = e0 + u * (int)blockDim.x + (int)threadIdx.x;
-          v[u] = 0;
-          if (e < nsoff) {
-            const int r = e / ncell, i = e - r * ncell;
-            int dy, dz;
-            run_dydz(r, dy, dz);
-            const int yy = y + dy, zz = z + dz;
-            if (yy >= 0 && yy < G.g[1] && zz >= 0 && zz < G.g[2]) {
-              const int x = min(max(xa - sx + i, 0), G.g[0]);  // x = gx: row end
-              v[u] = start[(zz * G.g[1] + yy) * G.g[0] + x];
-            }
-          }
+      for (int r = 0; r < 9; ++r) {
+        int dy, dz;
+        run_dydz(r, dy, dz);
+        const int yy = y + dy, zz = z + dz;
+        v[r] = 0;
+        if (i < ncell && yy >= 0 && yy < G.g[1] && zz >= 0 && zz < G.g[2]) {
+          const int x = min(max(xa - sx + i, 0), G.g[0]);  // x = gx: row end
+          v[r] = start[(zz * G.g[1] + yy) * G.g[0] + x];
         }
+      }
+      if (i < ncell) {
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-          const int e = e0 + u * (int)blockDim.x + (int)threadIdx.x;
-          if (e < nsoff) (&soff[0][0])[(e / ncell) * kTileCols + e % ncell] = v[u];
-        }
+        for (int r = 0; r < 9; ++r) soff[r][i] = v[r];
       }
     }
     __syncthreads();
@@ -2821,43 +2825,45 @@ __global__ __launch_bounds__(kTileThreads, NAVGPU_KNN_MINW) NAVGPU_KNN_ATTR void
       }
       __syncthreads();
       const int jmax = ncol - 1;
-      constexpr int U = NAVGPU_STAGE_U;  // records per thread per batch
-      for (int e0 = 0; e0 < total; e0 += U * (int)blockDim.x) {
-        Rec16 v[U];
-        int gg[U], rr[U];
+      // each wave copies whole row segments (r = wave, wave + nwaves, ...):
+      // r is wave-uniform, so a record's global position is e + s0[r] with
+      // no per-record segment decode (that decode was most of the staging
+      // VALU); a batch's loads are all issued before any LDS write
+      const int lane = (int)threadIdx.x & (kWave - 1);
+      const int nwv = (int)blockDim.x / kWave;
+      constexpr int U = NAVGPU_STAGE_U;  // records per lane per batch
+      for (int r = (int)threadIdx.x / kWave; r < 9; r += nwv) {
+        const int g0 = sb[r] + s0[r], nr = sb[r + 1] - sb[r];
+        const int *cb = &soff[r][0];
+        for (int k0 = 0; k0 < nr; k0 += U * kWave) {
+          Rec16 v[U];
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-          const int e = e0 + u * (int)blockDim.x + (int)threadIdx.x;
-          int g = e + s0[0], r = 0;
-#pragma unroll
-          for (int w = 1; w < 9; ++w) {
-            g = e >= sb[w] ? e + s0[w] : g;
-            r = e >= sb[w] ? w : r;
-          }
-          gg[u] = g;
-          rr[u] = r;
-          if (e < total) {
+          for (int u = 0; u < U; ++u) {
+            const int k = k0 + u * kWave + lane;
+            if (k < nr) {
 #ifdef NAVGPU_DBG_NOSTAGE  // timing-only ablation: no record loads
-            v[u].x = v[u].y = v[u].z = (float)g;
-            v[u].cx = xa;
+              v[u].x = v[u].y = v[u].z = (float)k;
+              v[u].cx = xa;
 #else
-            v[u] = rec[g];
+              v[u] = rec[g0 + k];
 #endif
+            }
           }
-        }
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-          const int e = e0 + u * (int)blockDim.x + (int)threadIdx.x;
-          if (e < total) {
-            // the record's column (its cell lies in xa-sx .. xb+sx; clamped
-            // so that a corrupt value cannot address outside the tile)
-            const int jj = min(max(v[u].cx - xa + sx, 0), jmax);
-            const int slot = soff[rr[u]][jj] + gg[u];
-            float *d = spair + (slot >> 1) * 4 + (slot & 1);
-            d[0] = v[u].x;
-            d[2] = v[u].y;
-            d[kZgOff] = v[u].z;
-            d[kZgOff + 2] = __int_as_float(gg[u]);
+          for (int u = 0; u < U; ++u) {
+            const int k = k0 + u * kWave + lane;
+            if (k < nr) {
+              // the record's column (its cell lies in xa-sx .. xb+sx; clamped
+              // so that a corrupt value cannot address outside the tile)
+              const int g = g0 + k;
+              const int jj = min(max(v[u].cx - xa + sx, 0), jmax);
+              const int slot = cb[jj] + g;
+              float *d = spair + (slot >> 1) * 4 + (slot & 1);
+              d[0] = v[u].x;
+              d[2] = v[u].y;
+              d[kZgOff] = v[u].z;
+              d[kZgOff + 2] = __int_as_float(g);
+            }
           }
         }
       }
