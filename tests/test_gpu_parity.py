@@ -112,6 +112,22 @@ def test_kd_build_million_level_parallel(gpu, orc, n, depth0, integer):
     _eq(gpu.kd_build(pts, depth0), np.roll(t, depth0, axis=1), f"n={n} depth0={depth0}")
 
 
+def test_kd_build_adversarial_orders(gpu, orc):
+    """Inputs on which Lomuto's last-element pivot degenerates: a tree-ordered
+    array (the output of a previous build) and an x-sorted one. These give
+    the grid-wide passes long tape chains (the jump rounds and the scatter's
+    own chain following) and hundreds of quickselect steps per level."""
+    rng = np.random.default_rng(31)
+    pts = rng.uniform(0, 1000, (150_000, 3))
+    tree, _ = orc.kd_build(pts)
+    t2, _ = orc.kd_build(tree.copy())
+    _eq(gpu.kd_build(tree), t2, "tree-ordered input")
+    s = rng.uniform(0, 1000, (20_000, 3))
+    s = s[np.argsort(s[:, 0], kind="stable")]
+    ts, _ = orc.kd_build(s.copy())
+    _eq(gpu.kd_build(s), ts, "x-sorted input")
+
+
 def test_kd_build_level_parallel_equals_single_workgroup(gpu, monkeypatch):
     rng = np.random.default_rng(9)
     pts = np.round(rng.uniform(0, 300, (40000, 3)))
