@@ -4125,7 +4125,7 @@ static int knn_run(navgpu_ctx *ctx, const double *tgt, size_t nt, const double *
                       ? ctx->knn_blocks
                       : (int)std::min<size_t>(768, std::max<size_t>(1, nq / 1300 + 1));
   const dim3 g(8 * nbx), b(kTileThreads);
-  const dim3 go(8 * std::min(nbx, 32));  // overflow tiles: rare, few blocks
+  const dim3 go(8 * std::min(nbx, 4));  // overflow tiles: rare, few blocks (an empty pass is launch cost only)
   const dim3 gs(std::max<unsigned>(1, std::min<unsigned>(2048, grid1d(nq, 256))));
 #define KNN_CASE(KK)                                                              \
   case KK:                                                                        \
