@@ -15,11 +15,11 @@
  *         exact KD permutation (src/slam.c:64-81, utils/kdtree.c:20-82), and
  *         the per-feature 1-NN batch (src/slam.c:236-244, utils/kdtree.c:
  *         110-152).
- *   host: the correspondence dedup and the 3-DOF Adam loop
- *         (src/slam.c:247-389): a sequential floating-point sum whose
- *         rounding order is part of the result, kept bit-identical here
- *         (dedup by hash instead of the reference's O(F^2) scan, same
- *         first-insertion order and keep-smaller-distance rule).
+ *         The correspondence list (src/slam.c:247-284) is built on the GPU
+ *         in the reference's first-insertion order; only the list comes back.
+ *   host: the 3-DOF Adam loop (src/slam.c:300-389), a sequential
+ *         floating-point sum whose rounding order is part of the result,
+ *         kept bit-identical here. NAVSLAM_ADAM=fast: GPU sums + closed form.
  * There is no CPU fallback for the GPU part: a device failure prints the
  * error and aborts (the reference API has no status codes).
  */
