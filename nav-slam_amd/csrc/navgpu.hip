@@ -116,13 +116,7 @@ __device__ __forceinline__ double ref_dist(double ax, double ay, double az,
 // (k = -2, -1, +1, +2 in that order). The four distances are computed once
 // and reused for the variance: sqrt is deterministic, so this is the
 // reference's second loop bit for bit.
-__device__ __forceinline__ double curvature5(const double *c, const double *m2,
-                                             const double *m1, const double *p1,
-                                             const double *p2) {
-  const double d0 = ref_dist(c[0], c[1], c[2], m2[0], m2[1], m2[2]);
-  const double d1 = ref_dist(c[0], c[1], c[2], m1[0], m1[1], m1[2]);
-  const double d2 = ref_dist(c[0], c[1], c[2], p1[0], p1[1], p1[2]);
-  const double d3 = ref_dist(c[0], c[1], c[2], p2[0], p2[1], p2[2]);
+__device__ __forceinline__ double curvature_of(double d0, double d1, double d2, double d3) {
   double sum = 0.0;
   sum += d0;
   sum += d1;
@@ -140,6 +134,15 @@ __device__ __forceinline__ double curvature5(const double *c, const double *m2,
     curv = var / count / (avg * avg + 1e-6f);
   }
   return curv;
+}
+
+__device__ __forceinline__ double curvature5(const double *c, const double *m2,
+                                             const double *m1, const double *p1,
+                                             const double *p2) {
+  return curvature_of(ref_dist(c[0], c[1], c[2], m2[0], m2[1], m2[2]),
+                      ref_dist(c[0], c[1], c[2], m1[0], m1[1], m1[2]),
+                      ref_dist(c[0], c[1], c[2], p1[0], p1[1], p1[2]),
+                      ref_dist(c[0], c[1], c[2], p2[0], p2[1], p2[2]));
 }
 
 // curvature of column j of a row held AoS in LDS (raw[3*j..]); 0 outside the
@@ -636,8 +639,14 @@ struct CurvJob {
   double *curv[2];
 };
 
+// Each neighbour distance serves two points: d(i, i+1) is point i's p1
+// distance and point i+1's m1 distance, d(i, i+2) point i's p2 and point
+// i+2's m2 (|a - b| squares to the same bits as |b - a|), so the tile
+// computes the two forward distances of every staged point once, in LDS,
+// and each point reads its four: two sqrt per point instead of four.
 __global__ __launch_bounds__(kCurvTile) void k_curvature(CurvJob J, int R, int C) {
   __shared__ double tile[3 * (kCurvTile + 4)];
+  __shared__ double dA[kCurvTile + 4], dB[kCurvTile + 4];  // d(i, i+1), d(i, i+2)
   const int z = blockIdx.z;
   const double *pts = J.pts[z];
   const int r = blockIdx.y;
@@ -645,14 +654,22 @@ __global__ __launch_bounds__(kCurvTile) void k_curvature(CurvJob J, int R, int C
   const int lo = max(0, c0 - 2), hi = min(C, c0 + kCurvTile + 2);
   const size_t rowoff = (size_t)r * C;
   const double *src = pts + 3 * (rowoff + lo);
-  const int nd = 3 * (hi - lo);
+  const int n = hi - lo, nd = 3 * n;
   for (int i = threadIdx.x; i < nd; i += kCurvTile) tile[i] = src[i];
   __syncthreads();
+  for (int i = threadIdx.x; i < n; i += kCurvTile) {
+    const double *a = tile + 3 * i;
+    if (i + 1 < n) dA[i] = ref_dist(a[0], a[1], a[2], a[3], a[4], a[5]);
+    if (i + 2 < n) dB[i] = ref_dist(a[0], a[1], a[2], a[6], a[7], a[8]);
+  }
+  __syncthreads();
   const int j = c0 + threadIdx.x;
-  const double *t = tile + 3 * (j - lo);
   if (j >= C) return;
   double cv = 0.0;
-  if (j >= 2 && j < C - 2) cv = curvature5(t, t - 6, t - 3, t + 3, t + 6);
+  if (j >= 2 && j < C - 2) {  // src/slam.c:16-58: k = -2, -1, +1, +2
+    const int i = j - lo;
+    cv = curvature_of(dB[i - 2], dA[i - 1], dA[i], dB[i]);
+  }
   J.mask[z][rowoff + j] = cv > 0.1 ? 1 : 0;
   if (J.curv[z]) J.curv[z][rowoff + j] = cv;
 }
