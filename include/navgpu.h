@@ -203,6 +203,14 @@ int navgpu_upload(navgpu_ctx *ctx, void *dst_dev, const void *src_host,
 int navgpu_download(navgpu_ctx *ctx, void *dst_host, const void *src_dev,
                     size_t bytes);
 
+/* Copies that overlap later work: navgpu_side_mark records the current
+ * point of the context's stream; navgpu_side_download copies device->host on
+ * a side stream once that point is reached, while work enqueued after the
+ * mark keeps running on the main stream. navgpu_sync waits for both. */
+int navgpu_side_mark(navgpu_ctx *ctx);
+int navgpu_side_download(navgpu_ctx *ctx, void *dst_host, const void *src_dev,
+                         size_t bytes);
+
 /* Kernel-level timing hook for bench.py: HIP events recorded around the
  * dominant kernel of the last *_dev call on the context's stream. Returns
  * the summed milliseconds of the named kernel since the last reset

@@ -3404,6 +3404,33 @@ void *navgpu_stream(navgpu_ctx *ctx) { return ctx ? (void *)ctx->stream : nullpt
 int navgpu_sync(navgpu_ctx *ctx) {
   ARG_CHECK(ctx);
   HIP_TRY(hipStreamSynchronize(ctx->stream));
+  if (ctx->aux) HIP_TRY(hipStreamSynchronize(ctx->aux));
+  return NAVGPU_OK;
+}
+
+static int ensure_aux(navgpu_ctx *ctx) {
+  if (!ctx->aux) {
+    HIP_TRY(hipStreamCreateWithFlags(&ctx->aux, hipStreamNonBlocking));
+    HIP_TRY(hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming));
+    HIP_TRY(hipEventCreateWithFlags(&ctx->ev_join, hipEventDisableTiming));
+  }
+  return NAVGPU_OK;
+}
+
+int navgpu_side_mark(navgpu_ctx *ctx) {
+  ARG_CHECK(ctx);
+  RC(ensure_aux(ctx));
+  HIP_TRY(hipEventRecord(ctx->ev_fork, ctx->stream));
+  return NAVGPU_OK;
+}
+
+int navgpu_side_download(navgpu_ctx *ctx, void *dst, const void *src, size_t bytes) {
+  ARG_CHECK(ctx);
+  if (!bytes) return NAVGPU_OK;
+  ARG_CHECK(dst && src);
+  RC(ensure_aux(ctx));
+  HIP_TRY(hipStreamWaitEvent(ctx->aux, ctx->ev_fork, 0));
+  HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, ctx->aux));
   return NAVGPU_OK;
 }
 

@@ -330,10 +330,12 @@ static void map_frame(SLAM_attr *attr, slam_state *s, Pos pos,
     attr->globalPointCloud[slot].ToF_timestamps = lidar->ToF_timestamps;
     CK(navgpu_upload(c, s->d_lidar, &lidar->ToF_position[0][0], 24 * NPTS));
     CK(navgpu_transform_dev(c, s->d_lidar, NPTS, R, t, NULL, s->d_global, NULL));
+    CK(navgpu_side_mark(c)); /* the map slot is final here */
     CK(navgpu_kd_build_rows_dev(c, s->d_lidar, s->d_global, ROWS, COLS,
                                 s->d_tree, s->d_tcol, s->d_tn, NULL));
-    CK(navgpu_download(c, &attr->globalPointCloud[slot].ToF_position[0][0],
-                       s->d_global, 24 * NPTS));
+    /* the map slot comes back while the trees build */
+    CK(navgpu_side_download(c, &attr->globalPointCloud[slot].ToF_position[0][0],
+                            s->d_global, 24 * NPTS));
     CK(navgpu_download(c, s->h_tree, s->d_tree, 24 * NPTS));
     CK(navgpu_download(c, s->h_tn, s->d_tn, 4 * ROWS));
     CK(navgpu_sync(c));

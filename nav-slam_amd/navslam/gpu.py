@@ -64,6 +64,8 @@ def _declare(L):
         "navgpu_free": (None, [_vp, _vp]),
         "navgpu_upload": (C.c_int, [_vp, _vp, _vp, _sz]),
         "navgpu_download": (C.c_int, [_vp, _vp, _vp, _sz]),
+        "navgpu_side_mark": (C.c_int, [_vp]),
+        "navgpu_side_download": (C.c_int, [_vp, _vp, _vp, _sz]),
         "navgpu_timing_enable": (None, [_vp, C.c_int]),
         "navgpu_timing_read": (C.c_double, [_vp, C.c_char_p, C.c_int]),
         "navgpu_timing_count": (C.c_int, [_vp, C.c_char_p]),
