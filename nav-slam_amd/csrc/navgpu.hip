@@ -944,7 +944,10 @@ __global__ __launch_bounds__(NT) void k_rows_match_lean(
 // kTiePending and its split flags the row; the tie pass (k_rows_match /
 // k_rows_match_lean with `tie`) builds the reference tree for those rows only.
 // Masks come from k_curvature; tie[r*S + split] is written by every split.
-constexpr int kScreenChunk = 32;
+#ifndef NAVGPU_SCREEN_CHUNK
+#define NAVGPU_SCREEN_CHUNK 32
+#endif
+constexpr int kScreenChunk = NAVGPU_SCREEN_CHUNK;
 
 __host__ __device__ inline int rows_screen_lds(int C, int w) {
   const int cp = (C + kScreenChunk - 1) / kScreenChunk * kScreenChunk;
@@ -1055,11 +1058,12 @@ __global__ __launch_bounds__(NT) void k_rows_screen(
   for (int e = n + (int)threadIdx.x; e < nch * kScreenChunk; e += NT)
     TX[e] = TY[e] = TZ[e] = INFINITY;
   // chunk bounding boxes (NaN coordinates left out: such a point's distance
-  // is NaN and never taken); two chunks per wave per pass, one per half-wave
+  // is NaN and never taken); 64 / kScreenChunk chunks per wave per pass
   const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
-  constexpr int NW = NT / kWave;
-  for (int b0 = 2 * wid; b0 < nch; b0 += 2 * NW) {
-    const int b = b0 + (lane >> 5), e = b * kScreenChunk + (lane & 31);
+  constexpr int NW = NT / kWave, CPW = kWave / kScreenChunk;
+  static_assert(kWave % kScreenChunk == 0, "chunks tile a wave");
+  for (int b0 = CPW * wid; b0 < nch; b0 += CPW * NW) {
+    const int b = b0 + lane / kScreenChunk, e = b * kScreenChunk + lane % kScreenChunk;
     const bool in = b < nch && e < n;
     double lo[3], hi[3];
     const double v[3] = {in ? TX[e] : NAN, in ? TY[e] : NAN, in ? TZ[e] : NAN};
@@ -1070,14 +1074,14 @@ __global__ __launch_bounds__(NT) void k_rows_screen(
       hi[a] = ok ? v[a] : -INFINITY;
     }
 #pragma unroll
-    for (int o = 16; o > 0; o >>= 1) {
+    for (int o = kScreenChunk / 2; o > 0; o >>= 1) {
 #pragma unroll
       for (int a = 0; a < 3; ++a) {
         lo[a] = fmin(lo[a], __shfl_xor(lo[a], o, kWave));
         hi[a] = fmax(hi[a], __shfl_xor(hi[a], o, kWave));
       }
     }
-    if (b < nch && (lane & 31) == 0) {
+    if (b < nch && lane % kScreenChunk == 0) {
       double *bx = BOX + 6 * b;
       bx[0] = lo[0];
       bx[1] = hi[0];

@@ -1,6 +1,7 @@
 """Time rows_match (screened per-row path) over screen launch knobs
 (NAVGPU_SCREEN_S / NAVGPU_SCREEN_NT are read per call) on the K2 pair and a
 K4-style batch; prints one line per configuration."""
+import argparse
 import os
 import sys
 import time
@@ -10,8 +11,15 @@ sys.path[:0] = [os.path.join(ROOT, "nav-slam_amd"), ROOT]
 import torch  # noqa: E402
 
 from navslam import synth  # noqa: E402
-from navslam.gpu import NavGpu  # noqa: E402
+import navslam.gpu as G  # noqa: E402
 
+ap = argparse.ArgumentParser()
+ap.add_argument("--lib", default=None)
+ap.add_argument("--default-only", action="store_true")
+args = ap.parse_args()
+if args.lib:
+    G.load_library(args.lib)
+NavGpu = G.NavGpu
 dev = torch.device("cuda", 0)
 g = NavGpu(0)
 g.timing(True)
@@ -25,8 +33,10 @@ def run(P, reps, label):
     i32 = lambda: torch.empty((P, R, Cc), dtype=torch.int32, device=dev)  # noqa: E731
     sm, tm, idx = i32(), i32(), i32()
     dst = torch.empty((P, R, Cc), dtype=torch.float64, device=dev)
-    for s_, nt in [(None, None), ("1", None), ("2", None), ("4", None), ("8", None),
-                   ("16", None), ("2", "512"), ("4", "512"), ("1", "512")]:
+    confs = [(None, None)] if args.default_only else [
+        (None, None), ("1", None), ("2", None), ("4", None), ("8", None), ("16", None),
+        ("2", "512"), ("4", "512"), ("1", "512")]
+    for s_, nt in confs:
         for k, v in (("NAVGPU_SCREEN_S", s_), ("NAVGPU_SCREEN_NT", nt)):
             if v is None:
                 os.environ.pop(k, None)
