@@ -189,8 +189,11 @@ int navgpu_pair_knn_dev(navgpu_ctx *ctx, const double *src, const double *tgt,
 /* ---- R5 for one arbitrary point array (kdtree.h buildKDTree) ------------
  * pts: n points (AoS), permuted in place into the reference's buildKDTree
  * order for a root at depth `depth0` (axis = (depth0 + level) % 3).
- * n up to INT32_MAX; rows that fit the LDS build in LDS, larger arrays use a
- * global-memory scratch of the same algorithm. */
+ * n < 2^30. Up to ~5.7k points the build runs in one workgroup's LDS.
+ * Larger arrays run the reference's Lomuto passes grid-wide, level by level
+ * (DESIGN.md §4). The number of quickselect rounds depends on the data, so
+ * that path reads a device flag back every 4 rounds: unlike the other
+ * *_dev calls it synchronises the host with the context's stream. */
 int navgpu_kd_build_dev(navgpu_ctx *ctx, double *pts, size_t n, int depth0);
 int navgpu_kd_build_host(navgpu_ctx *ctx, double *pts, size_t n, int depth0);
 
