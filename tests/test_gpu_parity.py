@@ -216,6 +216,29 @@ def test_rows_match_batch_lean_path(gpu, orc, monkeypatch):
             _eq(x[p], y, f"pair {p} {name}")
 
 
+def test_rows_match_dev_without_masks(gpu, orc):
+    """navgpu_rows_match_dev with NULL masks (the screen then keeps its masks
+    in the context's workspace), odd widths (C not a multiple of the 32-point
+    screen chunk, single-split and multi-split launches): the same matches as
+    the oracle."""
+    import torch
+    from navslam.synth import l9_pair
+    dev = torch.device("cuda", 0)
+    for R, Cc, seed in ((7, 37, 1), (40, 1000, 2), (130, 777, 3)):
+        a, b = l9_pair(R, Cc, seed=seed, integer_mm=seed == 2)
+        src, tgt = torch.from_numpy(a).to(dev), torch.from_numpy(b).to(dev)
+        idx = torch.full((R, Cc), -7, dtype=torch.int32, device=dev)
+        dist = torch.zeros((R, Cc), dtype=torch.float64, device=dev)
+        rc = gpu.L.navgpu_rows_match_dev(gpu.h, C.c_void_p(src.data_ptr()),
+                                         C.c_void_p(tgt.data_ptr()), R, Cc, None, None,
+                                         C.c_void_p(idx.data_ptr()), C.c_void_p(dist.data_ptr()))
+        assert rc == 0
+        torch.cuda.synchronize()
+        ref = orc.rows_match(a, b)
+        _eq(idx.cpu().numpy(), ref[2], f"{R}x{Cc} nn_idx")
+        _eq(dist.cpu().numpy(), ref[3], f"{R}x{Cc} nn_dist")
+
+
 def test_rows_match_edge_cases(gpu, orc):
     rng = np.random.default_rng(5)
     cases = [np.zeros((3, 5, 3)),                                   # C < 5: no window
