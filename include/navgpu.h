@@ -106,8 +106,10 @@ int navgpu_kd_build_rows_dev(navgpu_ctx *ctx, const double *feat_src,
  * Queries = feature points of `feat_src` (mask via R1), coordinates from
  * `queries`; query (r,c) searches tree r exactly like
  * nearestNeighborSearch (first-visited point wins ties). Per grid cell:
- *   nn_pos[r*C+c]  = tree position (index into row r of tree_pts), -1 if
- *                    (r,c) is not a feature or tree r is empty;
+ *   nn_pos[r*C+c]  = tree position (index into row r of tree_pts) holding
+ *                    the reference's answer Point (for bit-identical
+ *                    duplicates, the lowest position with those coordinates),
+ *                    -1 if (r,c) is not a feature or tree r is empty;
  *   nn_dist[r*C+c] = reference distance, +INFINITY when nn_pos == -1.
  * mask_out (nullable) receives the query feature mask. */
 int navgpu_kd_query_rows_dev(navgpu_ctx *ctx, const double *tree_pts,

@@ -1019,6 +1019,155 @@ __device__ int compact_cols(int c0, int c1, const int32_t *__restrict__ mask, Lo
   return base;
 }
 
+// One row's target points in LDS for the exact screen: SoA, padded with
+// +inf to whole chunks, with the chunks' bounding boxes.
+struct ScreenSet {
+  const double *TX, *TY, *TZ, *BOX;
+  int nch;
+};
+
+// lower bound of the computed dsq between any point of box bx and any query
+// of [qlo, qhi] (one query: qlo = qhi): each |fl(p - q)| >= fl(gap) by
+// monotone rounding, the same association
+__device__ __forceinline__ double screen_box_lb(const double *bx, double qlx, double qhx,
+                                                double qly, double qhy, double qlz,
+                                                double qhz) {
+  const double gx = fmax(fmax(bx[0] - qhx, qlx - bx[1]), 0.0);
+  const double gy = fmax(fmax(bx[2] - qhy, qly - bx[3]), 0.0);
+  const double gz = fmax(fmax(bx[4] - qhz, qlz - bx[5]), 0.0);
+  return gx * gx + gy * gy + gz * gz;
+}
+
+// Chunk boxes of TX/TY/TZ[0, n) (NaN coordinates left out: such a point's
+// distance is NaN and never taken); 64 / kScreenChunk chunks per wave per
+// pass. The caller synchronises before the boxes are read.
+template <int NT>
+__device__ void screen_boxes(const double *TX, const double *TY, const double *TZ,
+                             double *BOX, int n, int nch) {
+  const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
+  constexpr int NW = NT / kWave, CPW = kWave / kScreenChunk;
+  static_assert(kWave % kScreenChunk == 0, "chunks tile a wave");
+  for (int b0 = CPW * wid; b0 < nch; b0 += CPW * NW) {
+    const int b = b0 + lane / kScreenChunk, e = b * kScreenChunk + lane % kScreenChunk;
+    const bool in = b < nch && e < n;
+    double lo[3], hi[3];
+    const double v[3] = {in ? TX[e] : NAN, in ? TY[e] : NAN, in ? TZ[e] : NAN};
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+      const bool ok = v[a] == v[a];
+      lo[a] = ok ? v[a] : INFINITY;
+      hi[a] = ok ? v[a] : -INFINITY;
+    }
+#pragma unroll
+    for (int o = kScreenChunk / 2; o > 0; o >>= 1) {
+#pragma unroll
+      for (int a = 0; a < 3; ++a) {
+        lo[a] = fmin(lo[a], __shfl_xor(lo[a], o, kWave));
+        hi[a] = fmax(hi[a], __shfl_xor(hi[a], o, kWave));
+      }
+    }
+    if (b < nch && lane % kScreenChunk == 0) {
+      double *bx = BOX + 6 * b;
+      bx[0] = lo[0];
+      bx[1] = hi[0];
+      bx[2] = lo[1];
+      bx[3] = hi[1];
+      bx[4] = lo[2];
+      bx[5] = hi[2];
+    }
+  }
+}
+
+// The exact screen of one query per lane (called by whole waves): the
+// minimum d1 at position j1 and the runner-up d2 of the reference dsq over
+// the set. bound2 >= the final runner-up (e.g. the second smallest dsq of
+// any subset) prunes chunks before the scan has found two. Chunks s0
+// and s1 (wave-uniform, -1: none) are scanned first; then a lane per chunk
+// tests the chunk's box against the box of the wave's queries and the
+// largest runner-up of its lanes, and only chunks that pass get the
+// per-query test and the scan.
+__device__ void screen_query(const ScreenSet &T, bool act, double qx, double qy, double qz,
+                             int s0, int s1, double &d1, double &d2, int &j1,
+                             double bound2 = INFINITY) {
+  const int lane = threadIdx.x & (kWave - 1);
+  auto scan_chunk = [&](int k) {
+    NV_STAMP_ADD(13, 0ull, 1ull);
+    const int e0 = k * kScreenChunk;
+#pragma unroll 8
+    for (int u = 0; u < kScreenChunk; ++u) {
+      const int e = e0 + u;
+      const double dx = T.TX[e] - qx, dy = T.TY[e] - qy, dz = T.TZ[e] - qz;
+      const double d = dx * dx + dy * dy + dz * dz;  // utils/kdtree.c:16
+      j1 = d < d1 ? e : j1;
+      d2 = fmin(d2, fmax(d1, d));  // a NaN d makes d2 = d1: a (safe) tie
+      d1 = fmin(d1, d);
+    }
+  };
+  if (s0 >= 0) scan_chunk(s0);
+  if (s1 >= 0 && s1 != s0) scan_chunk(s1);
+  const bool qok = act && qx == qx && qy == qy && qz == qz;  // NaN: never matches
+  double wl[3] = {qok ? qx : INFINITY, qok ? qy : INFINITY, qok ? qz : INFINITY};
+  double wh[3] = {qok ? qx : -INFINITY, qok ? qy : -INFINITY, qok ? qz : -INFINITY};
+  double wd2 = qok ? fmin(d2, bound2) : -INFINITY;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+      wl[a] = fmin(wl[a], __shfl_xor(wl[a], o, kWave));
+      wh[a] = fmax(wh[a], __shfl_xor(wh[a], o, kWave));
+    }
+    wd2 = fmax(wd2, __shfl_xor(wd2, o, kWave));
+  }
+  for (int k0 = 0; k0 < T.nch; k0 += kWave) {
+    const int kl = k0 + lane;
+    bool pass = false;
+    if (kl < T.nch && kl != s0 && kl != s1)
+      pass = screen_box_lb(T.BOX + 6 * kl, wl[0], wh[0], wl[1], wh[1], wl[2], wh[2]) <= wd2;
+    unsigned long long m = __ballot(pass);
+    while (m) {
+      const int k = k0 + __builtin_ctzll(m);
+      m &= m - 1;
+      const double lb = screen_box_lb(T.BOX + 6 * k, qx, qx, qy, qy, qz, qz);
+      if (__any(act && lb <= fmin(d2, bound2))) scan_chunk(k);
+    }
+  }
+}
+
+// A runner-up at the minimum's distance (after sqrt, as the reference
+// compares) is a real tie only if some point in that distance band has
+// other coordinates: the reference returns a Point, so bit-identical
+// duplicates give the same answer whichever the tree visits first. Rare
+// (duplicated no-return points at the origin, integer data), so it is a
+// second pass over the chunks that can hold the band. Returns genuine (a
+// tie the tree must break) and emin, the lowest position of the duplicates.
+__device__ void screen_verify(const ScreenSet &T, bool act, double qx, double qy, double qz,
+                              double d1, double d2, int j1, bool &genuine, int &emin) {
+  const double dist = __builtin_sqrt(d1);
+  const bool suspect = act && d1 < INFINITY && __builtin_sqrt(d2) == dist;
+  genuine = false;
+  emin = j1;
+  if (!__any(suspect)) return;
+  const int jr = j1 >= 0 ? j1 : 0;
+  const long long rx = __double_as_longlong(T.TX[jr]), ry = __double_as_longlong(T.TY[jr]),
+                  rz = __double_as_longlong(T.TZ[jr]);
+  for (int k = 0; k < T.nch; ++k) {
+    const double lb = screen_box_lb(T.BOX + 6 * k, qx, qx, qy, qy, qz, qz);
+    if (!__any(suspect && __builtin_sqrt(lb) <= dist)) continue;
+    for (int u = 0; u < kScreenChunk; ++u) {
+      const int e = k * kScreenChunk + u;
+      const double dx = T.TX[e] - qx, dy = T.TY[e] - qy, dz = T.TZ[e] - qz;
+      const double d = dx * dx + dy * dy + dz * dz;
+      if (suspect && __builtin_sqrt(d) == dist) {
+        const bool same = __double_as_longlong(T.TX[e]) == rx &&
+                          __double_as_longlong(T.TY[e]) == ry &&
+                          __double_as_longlong(T.TZ[e]) == rz;
+        genuine |= !same;
+        emin = same ? min(emin, e) : emin;
+      }
+    }
+  }
+}
+
 template <int NT>
 __global__ __launch_bounds__(NT) void k_rows_screen(
     const double *__restrict__ src, const double *__restrict__ tgt, int R, int C,
@@ -1057,40 +1206,8 @@ __global__ __launch_bounds__(NT) void k_rows_screen(
   // the last chunk's tail: +inf coordinates, dsq = inf is never taken
   for (int e = n + (int)threadIdx.x; e < nch * kScreenChunk; e += NT)
     TX[e] = TY[e] = TZ[e] = INFINITY;
-  // chunk bounding boxes (NaN coordinates left out: such a point's distance
-  // is NaN and never taken); 64 / kScreenChunk chunks per wave per pass
   const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
-  constexpr int NW = NT / kWave, CPW = kWave / kScreenChunk;
-  static_assert(kWave % kScreenChunk == 0, "chunks tile a wave");
-  for (int b0 = CPW * wid; b0 < nch; b0 += CPW * NW) {
-    const int b = b0 + lane / kScreenChunk, e = b * kScreenChunk + lane % kScreenChunk;
-    const bool in = b < nch && e < n;
-    double lo[3], hi[3];
-    const double v[3] = {in ? TX[e] : NAN, in ? TY[e] : NAN, in ? TZ[e] : NAN};
-#pragma unroll
-    for (int a = 0; a < 3; ++a) {
-      const bool ok = v[a] == v[a];
-      lo[a] = ok ? v[a] : INFINITY;
-      hi[a] = ok ? v[a] : -INFINITY;
-    }
-#pragma unroll
-    for (int o = kScreenChunk / 2; o > 0; o >>= 1) {
-#pragma unroll
-      for (int a = 0; a < 3; ++a) {
-        lo[a] = fmin(lo[a], __shfl_xor(lo[a], o, kWave));
-        hi[a] = fmax(hi[a], __shfl_xor(hi[a], o, kWave));
-      }
-    }
-    if (b < nch && lane % kScreenChunk == 0) {
-      double *bx = BOX + 6 * b;
-      bx[0] = lo[0];
-      bx[1] = hi[0];
-      bx[2] = lo[1];
-      bx[3] = hi[1];
-      bx[4] = lo[2];
-      bx[5] = hi[2];
-    }
-  }
+  screen_boxes<NT>(TX, TY, TZ, BOX, n, nch);
   NV_STAMP(ss2);
   NV_STAMP_ADD(1, ss1, ss2);
   // this split's source features (block_compact synchronises, so the boxes
@@ -1116,98 +1233,18 @@ __global__ __launch_bounds__(NT) void k_rows_screen(
     const double qx = qp[0], qy = qp[1], qz = qp[2];
     // start at the chunk holding the first target feature at or after the
     // wave's first query column (scan rows are azimuth sweeps: the nearest
-    // point is usually a few columns away), then alternate outwards
+    // point is usually a few columns away)
     const int s = min((int)RANK[QL[i0]] / kScreenChunk, max(nch - 1, 0));
     double d1 = INFINITY, d2 = INFINITY;
     int j1 = -1;
-    auto scan_chunk = [&](int k) {
-      NV_STAMP_ADD(13, 0ull, 1ull);
-      const int e0 = k * kScreenChunk;
-#pragma unroll 8
-      for (int u = 0; u < kScreenChunk; ++u) {
-        const int e = e0 + u;
-        const double dx = TX[e] - qx, dy = TY[e] - qy, dz = TZ[e] - qz;
-        const double d = dx * dx + dy * dy + dz * dz;  // utils/kdtree.c:16
-        j1 = d < d1 ? e : j1;
-        d2 = fmin(d2, fmax(d1, d));  // a NaN d makes d2 = d1: a (safe) tie
-        d1 = fmin(d1, d);
-      }
-    };
-    // lower bound of the computed dsq between any point of box [lo, hi] and
-    // any query of [qlo, qhi] (a single query: qlo = qhi): each |fl(p - q)|
-    // >= fl(gap) by monotone rounding, the same association
-    auto box_lb = [](const double *bx, double qlx, double qhx, double qly, double qhy,
-                     double qlz, double qhz) {
-      const double gx = fmax(fmax(bx[0] - qhx, qlx - bx[1]), 0.0);
-      const double gy = fmax(fmax(bx[2] - qhy, qly - bx[3]), 0.0);
-      const double gz = fmax(fmax(bx[4] - qhz, qlz - bx[5]), 0.0);
-      return gx * gx + gy * gy + gz * gz;
-    };
-    // the two chunks where the wave's columns start (its queries' nearest
-    // points are usually there), unconditionally
-    const int s2 = min(s + 1, nch - 1);
-    if (nch > 0) scan_chunk(s);
-    if (s2 != s) scan_chunk(s2);
-    // then one test per CHUNK, a lane per chunk: the chunk's box against the
-    // box of the wave's queries and the largest runner-up of its lanes; only
-    // chunks that pass get the per-query test and the scan
-    const bool qok = act && qx == qx && qy == qy && qz == qz;  // NaN: never matches
-    double wl[3] = {qok ? qx : INFINITY, qok ? qy : INFINITY, qok ? qz : INFINITY};
-    double wh[3] = {qok ? qx : -INFINITY, qok ? qy : -INFINITY, qok ? qz : -INFINITY};
-    double wd2 = qok ? d2 : -INFINITY;
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-#pragma unroll
-      for (int a = 0; a < 3; ++a) {
-        wl[a] = fmin(wl[a], __shfl_xor(wl[a], o, kWave));
-        wh[a] = fmax(wh[a], __shfl_xor(wh[a], o, kWave));
-      }
-      wd2 = fmax(wd2, __shfl_xor(wd2, o, kWave));
-    }
-    for (int k0 = 0; k0 < nch; k0 += kWave) {
-      const int kl = k0 + lane;
-      bool pass = false;
-      if (kl < nch && kl != s && kl != s2)
-        pass = box_lb(BOX + 6 * kl, wl[0], wh[0], wl[1], wh[1], wl[2], wh[2]) <= wd2;
-      unsigned long long m = __ballot(pass);
-      while (m) {
-        const int k = k0 + __builtin_ctzll(m);
-        m &= m - 1;
-        const double lb = box_lb(BOX + 6 * k, qx, qx, qy, qy, qz, qz);
-        if (__any(act && lb <= d2)) scan_chunk(k);
-      }
-    }
+    const ScreenSet T = {TX, TY, TZ, BOX, nch};
+    // the two chunks where the wave's columns start, unconditionally
+    screen_query(T, act, qx, qy, qz, nch > 0 ? s : -1, nch > 0 ? min(s + 1, nch - 1) : -1,
+                 d1, d2, j1);
     const double dist = __builtin_sqrt(d1);
-    // a runner-up at the minimum's distance: a real tie only if some point
-    // in that distance band has other coordinates (the reference returns a
-    // Point, so bit-identical duplicates give the same answer whichever the
-    // tree visits first; nn_idx then names the lowest column among them).
-    // Rare (duplicated no-return points at the origin, integer data), so it
-    // is a second pass over the chunks that can hold the band.
-    const bool suspect = act && d1 < INFINITY && __builtin_sqrt(d2) == dist;
-    bool genuine = false;
-    int emin = j1;
-    if (__any(suspect)) {
-      const int jr = j1 >= 0 ? j1 : 0;
-      const long long rx = __double_as_longlong(TX[jr]), ry = __double_as_longlong(TY[jr]),
-                      rz = __double_as_longlong(TZ[jr]);
-      for (int k = 0; k < nch; ++k) {
-        const double lb = box_lb(BOX + 6 * k, qx, qx, qy, qy, qz, qz);
-        if (!__any(suspect && __builtin_sqrt(lb) <= dist)) continue;
-        for (int u = 0; u < kScreenChunk; ++u) {
-          const int e = k * kScreenChunk + u;
-          const double dx = TX[e] - qx, dy = TY[e] - qy, dz = TZ[e] - qz;
-          const double d = dx * dx + dy * dy + dz * dz;
-          if (suspect && __builtin_sqrt(d) == dist) {
-            const bool same = __double_as_longlong(TX[e]) == rx &&
-                              __double_as_longlong(TY[e]) == ry &&
-                              __double_as_longlong(TZ[e]) == rz;
-            genuine |= !same;
-            emin = same ? min(emin, e) : emin;
-          }
-        }
-      }
-    }
+    bool genuine;
+    int emin;
+    screen_verify(T, act, qx, qy, qz, d1, d2, j1, genuine, emin);
     if (act) {
       const bool t = genuine || (d1 < INFINITY && dist > 0.0 && dist < 1e-150);
       if (t) {
@@ -1297,6 +1334,125 @@ __global__ __launch_bounds__(kRowsQBlock) void k_rows_query(
     }
     nn_pos[rowoff + j] = bpos;
     nn_dist[rowoff + j] = bd;
+  }
+}
+
+// k_rows_query without the tree walk (default): the same answers from the
+// exact screen over the row's tree points (a set; the tree order only
+// decides duplicates, which give the same Point). Each lane first descends
+// the implicit tree without backtracking (the nodes on its path are real
+// candidates and seed the minimum and runner-up), then screen_query scans
+// the chunks that can still matter. Genuine ties (distinct points at the
+// minimum distance) and underflowing distances take kd_query, the
+// reference walk, on the same LDS tree. nn_pos is a position holding the
+// reference's answer (for bit-identical duplicates, the lowest such one).
+template <int NT>
+__global__ __launch_bounds__(NT) void k_rows_query_screen(
+    const double *__restrict__ tree_pts, const int32_t *__restrict__ tree_n,
+    const double *__restrict__ feat_src, const double *__restrict__ queries, int R, int C,
+    int32_t *__restrict__ nn_pos, double *__restrict__ nn_dist, int32_t *__restrict__ mask_out) {
+  const int r = blockIdx.x;
+  const int w = (C + (int)gridDim.y - 1) / (int)gridDim.y;
+  const int c0 = (int)blockIdx.y * w, c1 = min(C, c0 + w);
+  if (c0 >= c1) return;
+  const size_t rowoff = (size_t)r * C;
+  const int cp = (C + kScreenChunk - 1) / kScreenChunk * kScreenChunk;
+  double *TX = (double *)smem;
+  double *TY = (double *)(smem + align16(8 * cp));
+  double *TZ = (double *)(smem + 2 * align16(8 * cp));
+  double *BOX = (double *)(smem + 3 * align16(8 * cp));
+  double *rs = (double *)((unsigned char *)BOX + align16(48 * (cp / kScreenChunk)));
+  uint16_t *QL = (uint16_t *)((unsigned char *)rs + align16(24 * (w + 4)));
+  uint16_t *FL = QL + align16(2 * w) / 2;
+  int *scan = (int *)((unsigned char *)FL + align16(2 * w));
+  uint32_t *stk = (uint32_t *)((unsigned char *)scan + align16(4 * 40));
+  const int n = tree_n[r];
+  const int nch = (n + kScreenChunk - 1) / kScreenChunk;
+  for (int pos = threadIdx.x; pos < nch * kScreenChunk; pos += NT) {
+    if (pos < n) {
+      const double *t = tree_pts + 3 * (rowoff + pos);
+      TX[pos] = t[0];
+      TY[pos] = t[1];
+      TZ[pos] = t[2];
+    } else {
+      TX[pos] = TY[pos] = TZ[pos] = INFINITY;  // dsq = inf: never taken
+    }
+  }
+  const int lo = max(c0 - 2, 0), hi = min(c1 + 2, C);  // slice + curvature halo
+  block_copy(rs, feat_src + 3 * (rowoff + lo), 3 * (hi - lo));
+  __syncthreads();
+  screen_boxes<NT>(TX, TY, TZ, BOX, n, nch);
+  for (int j = c0 + (int)threadIdx.x; j < c1; j += NT) {
+    int f = 0;
+    if (j >= 2 && j < C - 2) {  // src/slam.c:16 window
+      const double *cj = rs + 3 * (j - lo);
+      f = curvature5(cj, cj - 6, cj - 3, cj + 3, cj + 6) > 0.1 ? 1 : 0;
+    }
+    FL[j - c0] = (uint16_t)f;
+    if (mask_out) mask_out[rowoff + j] = f;
+    if (!f) {
+      nn_pos[rowoff + j] = -1;
+      nn_dist[rowoff + j] = INFINITY;
+    }
+  }
+  __syncthreads();  // flags and boxes visible
+  const int nq = block_compact(
+      c1 - c0, scan, [&](int j) { return FL[j] != 0; },
+      [&](int j, int pos) { QL[pos] = (uint16_t)(c0 + j); });
+  const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
+  const ScreenSet T = {TX, TY, TZ, BOX, nch};
+  for (int i0 = wid * kWave; i0 < nq; i0 += NT) {  // wave-uniform trip count
+    const int i = i0 + lane;
+    const bool act = i < nq;
+    const int c = QL[act ? i : i0];
+    const double *qp = queries + 3 * (rowoff + c);
+    const double qx = qp[0], qy = qp[1], qz = qp[2];
+    // bound: the two smallest dsq on the path of a descent without
+    // backtracking (utils/kdtree.c:132-145's near branch at every node); the
+    // final runner-up can only be smaller. They are a bound only: the scan
+    // starts empty, so no point is counted twice (a point counted twice would
+    // look like a runner-up at the minimum's distance).
+    double e1 = INFINITY, e2 = INFINITY;
+    {
+      int a0 = 0, a1 = n, depth = 0;
+      while (a0 < a1) {
+        const int mid = a0 + ((a1 - a0) >> 1);
+        const double nx = TX[mid], ny = TY[mid], nz = TZ[mid];
+        const double dx = nx - qx, dy = ny - qy, dz = nz - qz;
+        const double d = dx * dx + dy * dy + dz * dz;
+        // explicit compares: a NaN d changes nothing (e2 must stay >= the
+        // true runner-up to be a safe pruning bound)
+        if (d < e1) {
+          e2 = e1;
+          e1 = d;
+        } else if (d < e2) {
+          e2 = d;
+        }
+        const int axis = depth % 3;
+        const double qa = axis == 0 ? qx : (axis == 1 ? qy : qz);
+        const double na = axis == 0 ? nx : (axis == 1 ? ny : nz);
+        if (qa < na)
+          a1 = mid;
+        else
+          a0 = mid + 1;
+        ++depth;
+      }
+    }
+    double d1 = INFINITY, d2 = INFINITY;
+    int j1 = -1;
+    screen_query(T, act, qx, qy, qz, -1, -1, d1, d2, j1, e2);
+    const double dist = __builtin_sqrt(d1);
+    bool genuine;
+    int emin;
+    screen_verify(T, act, qx, qy, qz, d1, d2, j1, genuine, emin);
+    if (act) {
+      int bpos = j1 >= 0 ? emin : -1;
+      double bd = j1 >= 0 ? dist : INFINITY;
+      if (genuine || (d1 < INFINITY && dist > 0.0 && dist < 1e-150))
+        kd_query(TX, TY, TZ, n, qx, qy, qz, stk + threadIdx.x, NT, &bpos, &bd);
+      nn_pos[rowoff + c] = bpos;
+      nn_dist[rowoff + c] = bd;
+    }
   }
 }
 
@@ -3677,8 +3833,32 @@ int navgpu_kd_query_rows_dev(navgpu_ctx *ctx, const double *tree_pts,
   RC(check_rows_shape(R, C, true));
   if ((size_t)R * C == 0) return NAVGPU_OK;
   ARG_CHECK(tree_pts && tree_n && feat_src && queries && nn_pos && nn_dist);
-  // column splits per row: >= 512 workgroups in all (2 per CU), slices of at
-  // least 256 columns (one per thread)
+  const char *qt = getenv("NAVGPU_ROWS_QUERY_TREE");
+  if (!(qt && *qt && *qt != '0')) {
+    // the screen (default): >= 1024 workgroups, >= 128 columns each (two
+    // ~74 KB workgroups per CU at C = 2048)
+    int S = 1;
+    while (S < 16 && (long long)R * S < 1024 && C / (2 * S) >= 128) S <<= 1;
+    const int w = (C + S - 1) / S;
+    const int cp = (C + kScreenChunk - 1) / kScreenChunk * kScreenChunk;
+    const int lds = 3 * align16(8 * cp) + align16(48 * (cp / kScreenChunk)) +
+                    align16(24 * (w + 4)) + 2 * align16(2 * w) + align16(4 * 40) +
+                    4 * kRowsQBlock * kStackDepth;
+    if (lds > lds_limit()) {
+      set_err("rows_query: C=%d needs %d B of LDS (device limit %d)", C, lds, lds_limit());
+      return NAVGPU_ERANGE;
+    }
+    RC(set_lds(k_rows_query_screen<kRowsQBlock>, lds));
+    TimedRegion tr(ctx, "rows_query");
+    hipLaunchKernelGGL(k_rows_query_screen<kRowsQBlock>, dim3(R, S), dim3(kRowsQBlock), lds,
+                       ctx->stream, tree_pts, tree_n, feat_src, queries, R, C, nn_pos, nn_dist,
+                       mask_out);
+    CHECK_LAUNCH("k_rows_query_screen");
+    return NAVGPU_OK;
+  }
+  // NAVGPU_ROWS_QUERY_TREE=1: the reference walk for every query. Column
+  // splits per row: >= 512 workgroups in all (2 per CU), slices of at least
+  // 256 columns (one per thread)
   int S = 1;
   while (S < 8 && (long long)R * S < 512 && C / (2 * S) >= kRowsQBlock) S <<= 1;
   const int w = (C + S - 1) / S;

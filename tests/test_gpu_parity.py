@@ -290,9 +290,14 @@ def test_rows_screen_vs_tree_path(gpu, orc, monkeypatch):
             _eq(a, c, f"{label}: screen vs oracle {name}")
 
 
-def test_split_build_query_vs_oracle(gpu, orc):
+@pytest.mark.parametrize("query_tree", ["0", "1"])
+def test_split_build_query_vs_oracle(gpu, orc, monkeypatch, query_tree):
     """kd_build_rows_dev + kd_query_rows_dev on device tensors (slam.c split:
-    features from the lidar frame, coordinates from a transformed frame)."""
+    features from the lidar frame, coordinates from a transformed frame).
+    The query returns the reference's Point: its position, or for
+    bit-identical duplicates a position holding the same coordinates; both
+    the screen (default) and the tree walk (NAVGPU_ROWS_QUERY_TREE=1)."""
+    monkeypatch.setenv("NAVGPU_ROWS_QUERY_TREE", query_tree)
     import torch
     from navslam.synth import l9_pair
     R, Cc = 64, 1024
@@ -327,7 +332,9 @@ def test_split_build_query_vs_oracle(gpu, orc):
         _eq(tcol[r, :len(cols)], cols[rix], f"row {r} cols")
         for c in np.nonzero(qm[r] == 1)[0]:
             p, d = orc.kd_nn(rt, lid2[r, c])
-            assert pos[r, c] == p and (dist[r, c] == d), (r, c)
+            assert (pos[r, c] >= 0) == (p >= 0) and dist[r, c] == d, (r, c)
+            if p >= 0:
+                assert tree[r, pos[r, c]].tobytes() == rt[p].tobytes(), (r, c)
         assert (pos[r][qm[r] == 0] == -1).all()
 
 
