@@ -102,6 +102,20 @@ int navgpu_kd_build_rows_dev(navgpu_ctx *ctx, const double *feat_src,
                              double *tree_pts, int32_t *tree_col,
                              int32_t *tree_n, int32_t *mask_out);
 
+/* ---- R5 host trees: KDNode images of the trees of navgpu_kd_build_rows ---
+ * Replaces the per-node malloc + linking of buildKDTree (utils/kdtree.c:
+ * 65-82) for the per-row trees of updateKDTree (src/slam.c:161-170).
+ * row_off (R+1 int32, device): row_off[r] = tree_n[0]+...+tree_n[r-1],
+ * row_off[R] = total. nodes (device, 40*total bytes): for row r and tree
+ * position i < tree_n[r], a kdtree.h KDNode {Point point; KDNode *left,
+ * *right} at nodes + 40*(row_off[r]+i) whose left/right are the host
+ * addresses host_base + 40*(row_off[r]+child) of its children in the
+ * implicit layout (NULL for none). Downloaded to host_base, row r's tree is
+ * rooted at host_base + 40*(row_off[r] + tree_n[r]/2). R <= 65535. */
+int navgpu_kd_rows_nodes_dev(navgpu_ctx *ctx, const double *tree_pts,
+                             const int32_t *tree_n, int R, int C,
+                             uint64_t host_base, void *nodes, int32_t *row_off);
+
 /* ---- R6: per-row 1-NN over the trees of navgpu_kd_build_rows ------------
  * Queries = feature points of `feat_src` (mask via R1), coordinates from
  * `queries`; query (r,c) searches tree r exactly like
@@ -202,6 +216,10 @@ int navgpu_kd_build_host(navgpu_ctx *ctx, double *pts, size_t n, int depth0);
 /* ---- device memory helpers (for C callers without HIP headers) --------- */
 int navgpu_malloc(navgpu_ctx *ctx, size_t bytes, void **dptr);
 void navgpu_free(navgpu_ctx *ctx, void *dptr);
+/* page-locked host memory (copies to and from it skip the staging buffer);
+ * navgpu_host_free waits for the context's streams first */
+int navgpu_host_alloc(navgpu_ctx *ctx, size_t bytes, void **hptr);
+void navgpu_host_free(navgpu_ctx *ctx, void *hptr);
 /* stream-ordered copies on the context's stream (host memory pageable) */
 int navgpu_upload(navgpu_ctx *ctx, void *dst_dev, const void *src_host,
                   size_t bytes);

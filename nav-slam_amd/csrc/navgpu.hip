@@ -1285,6 +1285,66 @@ __global__ __launch_bounds__(kRowsBlock) void k_rows_build(
   if (threadIdx.x == 0) tree_n[r] = n;
 }
 
+// Host KDNode images of the per-row trees (navgpu_kd_rows_nodes_dev).
+// off[r] = tree_n[0] + ... + tree_n[r-1], off[R] = total: one workgroup,
+// each thread a contiguous run of rows, then a scan of the run sums.
+constexpr int kOffBlock = 1024;
+__global__ __launch_bounds__(kOffBlock) void k_rows_offsets(
+    const int32_t *__restrict__ tree_n, int R, int32_t *__restrict__ off) {
+  __shared__ int32_t part[kOffBlock];
+  const int per = (R + kOffBlock - 1) / kOffBlock;
+  const int r0 = min(R, (int)threadIdx.x * per), r1 = min(R, r0 + per);
+  int32_t s = 0;
+  for (int r = r0; r < r1; ++r) s += tree_n[r];
+  part[threadIdx.x] = s;
+  __syncthreads();
+  for (int d = 1; d < kOffBlock; d <<= 1) {  // Hillis-Steele inclusive scan
+    const int32_t v = threadIdx.x >= (unsigned)d ? part[threadIdx.x - d] : 0;
+    __syncthreads();
+    part[threadIdx.x] += v;
+    __syncthreads();
+  }
+  int32_t acc = part[threadIdx.x] - s;
+  for (int r = r0; r < r1; ++r) {
+    off[r] = acc;
+    acc += tree_n[r];
+  }
+  if (threadIdx.x == kOffBlock - 1) off[R] = part[kOffBlock - 1];
+}
+
+// One thread per tree position: the node of position p in the implicit
+// layout (node of [lo,hi) at lo+(hi-lo)/2, utils/kdtree.c:65-82) found by
+// descending from the root, its children's host addresses written beside the
+// Point so that the image downloads straight into a KDNode array at host_base
+// (utils/kdtree.h:7-11: Point point; KDNode *left, *right — 40 bytes).
+__global__ __launch_bounds__(256) void k_rows_nodes(
+    const double *__restrict__ tree_pts, const int32_t *__restrict__ tree_n,
+    const int32_t *__restrict__ off, int C, uint64_t host_base,
+    uint64_t *__restrict__ nodes) {
+  const int r = blockIdx.y;
+  const int p = (int)blockIdx.x * blockDim.x + threadIdx.x;
+  const int n = tree_n[r];
+  if (p >= n) return;
+  int lo = 0, hi = n, mid = n >> 1;
+  while (mid != p) {
+    if (p < mid)
+      hi = mid;
+    else
+      lo = mid + 1;
+    mid = lo + ((hi - lo) >> 1);
+  }
+  const long long o = off[r];
+  const int left = lo < mid ? lo + ((mid - lo) >> 1) : -1;
+  const int right = mid + 1 < hi ? mid + 1 + ((hi - mid - 1) >> 1) : -1;
+  const double *t = tree_pts + 3 * ((size_t)r * C + p);
+  uint64_t *nd = nodes + 5 * (o + p);
+  nd[0] = __double_as_longlong(t[0]);
+  nd[1] = __double_as_longlong(t[1]);
+  nd[2] = __double_as_longlong(t[2]);
+  nd[3] = left < 0 ? 0 : host_base + 40ull * (uint64_t)(o + left);
+  nd[4] = right < 0 ? 0 : host_base + 40ull * (uint64_t)(o + right);
+}
+
 // Per-row 1-NN, each row's columns split over gridDim.y workgroups so a
 // frame of R rows fills the chip (R = 128 rows alone would occupy half the
 // CUs): every split loads the row's whole tree into LDS (SoA) and its own
@@ -3822,6 +3882,48 @@ int navgpu_kd_build_rows_dev(navgpu_ctx *ctx, const double *feat_src,
                      tree_n, mask_out);
   CHECK_LAUNCH("k_rows_build");
   return NAVGPU_OK;
+}
+
+int navgpu_kd_rows_nodes_dev(navgpu_ctx *ctx, const double *tree_pts,
+                             const int32_t *tree_n, int R, int C,
+                             uint64_t host_base, void *nodes, int32_t *row_off) {
+  ARG_CHECK(ctx);
+  RC(check_rows_shape(R, C, false));
+  ARG_CHECK(row_off);
+  if (R == 0) {
+    HIP_TRY(hipMemsetAsync(row_off, 0, 4, ctx->stream));
+    return NAVGPU_OK;
+  }
+  ARG_CHECK(tree_n && (C == 0 || (tree_pts && nodes)));
+  ARG_CHECK(R <= 65535);  // grid.y of k_rows_nodes
+  hipLaunchKernelGGL(k_rows_offsets, dim3(1), dim3(kOffBlock), 0, ctx->stream,
+                     tree_n, R, row_off);
+  CHECK_LAUNCH("k_rows_offsets");
+  if (C == 0) return NAVGPU_OK;
+  hipLaunchKernelGGL(k_rows_nodes, dim3((C + 255) / 256, R), dim3(256), 0,
+                     ctx->stream, tree_pts, tree_n, row_off, C, host_base,
+                     (uint64_t *)nodes);
+  CHECK_LAUNCH("k_rows_nodes");
+  return NAVGPU_OK;
+}
+
+int navgpu_host_alloc(navgpu_ctx *ctx, size_t bytes, void **hptr) {
+  ARG_CHECK(ctx && hptr);
+  *hptr = nullptr;
+  hipError_t e = hipHostMalloc(hptr, bytes ? bytes : 16, hipHostMallocDefault);
+  if (e != hipSuccess) {
+    set_err("hipHostMalloc(%zu): %s", bytes, hipGetErrorString(e));
+    *hptr = nullptr;
+    return NAVGPU_ENOMEM;
+  }
+  return NAVGPU_OK;
+}
+
+void navgpu_host_free(navgpu_ctx *ctx, void *hptr) {
+  if (!ctx || !hptr) return;
+  (void)hipStreamSynchronize(ctx->stream);
+  if (ctx->aux) (void)hipStreamSynchronize(ctx->aux);
+  (void)hipHostFree(hptr);
 }
 
 int navgpu_kd_query_rows_dev(navgpu_ctx *ctx, const double *tree_pts,

@@ -28,6 +28,8 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <stddef.h>
+#include <time.h>
 
 #include "navgpu.h"
 #include "slam.h"
@@ -62,6 +64,43 @@ static navgpu_ctx *ctx(void)
     }
     return g_ctx;
 }
+
+/* NAVSLAM_PROFILE=1: host-side phase times, printed at exit (diagnostic) */
+static double g_prof[8];
+static long g_prof_n[8];
+static int g_prof_on = -1;
+static double now_s(void)
+{
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return ts.tv_sec + 1e-9 * ts.tv_nsec;
+}
+static void prof_dump(void)
+{
+    static const char *names[8] = {"map: gpu+copies", "map: link trees", "loc: gpu+copies",
+                                   "loc: adam", "", "", "", ""};
+    for (int i = 0; i < 8; i++)
+        if (g_prof_n[i])
+            fprintf(stderr, "navslam profile %-18s %8.3f ms avg over %ld\n", names[i],
+                    1e3 * g_prof[i] / g_prof_n[i], g_prof_n[i]);
+}
+static int prof_on(void)
+{
+    if (g_prof_on < 0) {
+        const char *e = getenv("NAVSLAM_PROFILE");
+        g_prof_on = e && *e == '1';
+        if (g_prof_on)
+            atexit(prof_dump);
+    }
+    return g_prof_on;
+}
+#define PROF_ADD(i, t0)                     \
+    do {                                    \
+        if (prof_on()) {                    \
+            g_prof[i] += now_s() - (t0);    \
+            g_prof_n[i]++;                  \
+        }                                   \
+    } while (0)
 
 static int quiet(void)
 {
@@ -127,6 +166,27 @@ static KDNode *make_block(const Point *pts, size_t n)
     g_blocks[g_nblocks].n = n;
     g_nblocks++;
     return root;
+}
+
+/* A slab of row trees owned by a SLAM_attr's state (map_frame): freeKDTree
+ * on any node inside it is a no-op, the slab lives as long as the state. */
+_Static_assert(sizeof(KDNode) == 40 && offsetof(KDNode, left) == 24 &&
+                   offsetof(KDNode, right) == 32,
+               "KDNode layout of utils/kdtree.h:7-11 (navgpu_kd_rows_nodes_dev)");
+static void register_slab(KDNode *base, size_t n)
+{
+    if (g_nblocks == g_capblocks) {
+        g_capblocks = g_capblocks ? 2 * g_capblocks : 64;
+        g_blocks = realloc(g_blocks, sizeof(kd_block) * g_capblocks);
+    }
+    if (!g_blocks) {
+        fprintf(stderr, "navslam: out of host memory\n");
+        abort();
+    }
+    g_blocks[g_nblocks].root = NULL;
+    g_blocks[g_nblocks].base = base;
+    g_blocks[g_nblocks].n = n;
+    g_nblocks++;
 }
 
 static int release_block(KDNode *root)
@@ -265,9 +325,12 @@ typedef struct {
     double h_sums[6 * ROWS];
     int32_t *d_tcol, *d_tn, *d_pos, *d_count;
     int have_trees;
-    double h_tree[NPTS * 3];
-    int32_t h_tn[ROWS];
-    KDNode *roots[ROWS];
+    double prof_t0; /* NAVSLAM_PROFILE */
+    int32_t *d_off;         /* row offsets of the node image (ROWS+1) */
+    void *d_nodes;          /* KDNode image of the row trees, device */
+    KDNode *h_nodes;        /* its host copy: the trees handed out */
+    int h_nodes_pinned;
+    int32_t h_off[ROWS + 1];
     NeighborResult *result; /* correspondence list (src/slam.c:214) */
 } slam_state;
 
@@ -297,6 +360,19 @@ static slam_state *state_for(SLAM_attr *a)
     CK(navgpu_malloc(c, 8 * 6 * ROWS, (void **)&s->d_sums));
     CK(navgpu_malloc(c, 56 * (size_t)NPTS, (void **)&s->d_list));
     CK(navgpu_malloc(c, 8, (void **)&s->d_count));
+    CK(navgpu_malloc(c, 4 * (ROWS + 1), (void **)&s->d_off));
+    CK(navgpu_malloc(c, sizeof(KDNode) * (size_t)NPTS, &s->d_nodes));
+    /* page-locked when the runtime allows it: the image then downloads by
+     * DMA straight into the trees */
+    s->h_nodes_pinned =
+        navgpu_host_alloc(c, sizeof(KDNode) * (size_t)NPTS, (void **)&s->h_nodes) == 0;
+    if (!s->h_nodes_pinned)
+        s->h_nodes = malloc(sizeof(KDNode) * (NPTS ? (size_t)NPTS : 1));
+    if (!s->h_nodes) {
+        fprintf(stderr, "navslam: out of host memory\n");
+        abort();
+    }
+    register_slab(s->h_nodes, NPTS);
     g_states = realloc(g_states, sizeof(*g_states) * (g_nstates + 1));
     g_states[g_nstates++] = s;
     return s;
@@ -325,6 +401,7 @@ static void map_frame(SLAM_attr *attr, slam_state *s, Pos pos,
                       PointCloud *lidar, int slot)
 {
     navgpu_ctx *c = ctx();
+    const double pt0 = prof_on() ? now_s() : 0.0;
     double R[9], t[3] = {pos.x, pos.y, pos.z};
     rotation(pos.roll, pos.pitch, pos.yaw, R);
     attr->globalPointCloud[slot].ToF_timestamps = lidar->ToF_timestamps;
@@ -336,19 +413,36 @@ static void map_frame(SLAM_attr *attr, slam_state *s, Pos pos,
     /* the map slot comes back while the trees build */
     CK(navgpu_side_download(c, &attr->globalPointCloud[slot].ToF_position[0][0],
                             s->d_global, 24 * NPTS));
-    CK(navgpu_download(c, s->h_tree, s->d_tree, 24 * NPTS));
-    CK(navgpu_download(c, s->h_tn, s->d_tn, 4 * ROWS));
-    CK(navgpu_sync(c));
     s->have_trees = 1;
-    int ht = host_trees();
-    for (int r = 0; r < ROWS; r++) {
-        if (s->roots[r])
-            freeKDTree(s->roots[r]); /* the reference leaks these */
-        s->roots[r] = ht ? make_block((const Point *)(s->h_tree + 3 * (size_t)r * COLS),
-                                      (size_t)s->h_tn[r])
-                         : NULL;
-        attr->kdtree_lastframe[r] = s->roots[r];
+    if (!host_trees()) {
+        CK(navgpu_sync(c));
+        for (int r = 0; r < ROWS; r++)
+            attr->kdtree_lastframe[r] = NULL;
+        PROF_ADD(0, pt0);
+        return;
     }
+    /* the host trees: their linked KDNode image is written on the GPU with
+     * the slab's host addresses and lands in place (no per-node malloc or
+     * linking on the host). The slab is this state's: the previous frame's
+     * trees (which the reference leaks) are overwritten, not freed. */
+    CK(navgpu_kd_rows_nodes_dev(c, s->d_tree, s->d_tn, ROWS, COLS,
+                                (uint64_t)(uintptr_t)s->h_nodes, s->d_nodes, s->d_off));
+    CK(navgpu_download(c, s->h_off, s->d_off, sizeof(s->h_off)));
+    CK(navgpu_sync(c));
+    PROF_ADD(0, pt0);
+    const double pt1 = prof_on() ? now_s() : 0.0;
+    const int32_t total = s->h_off[ROWS];
+    if (total < 0 || total > NPTS) {
+        fprintf(stderr, "navslam: bad tree sizes from the device (%d)\n", (int)total);
+        abort();
+    }
+    CK(navgpu_download(c, s->h_nodes, s->d_nodes, sizeof(KDNode) * (size_t)total));
+    CK(navgpu_sync(c));
+    for (int r = 0; r < ROWS; r++) {
+        const int32_t n = s->h_off[r + 1] - s->h_off[r];
+        attr->kdtree_lastframe[r] = n > 0 ? s->h_nodes + s->h_off[r] + n / 2 : NULL;
+    }
+    PROF_ADD(1, pt1);
 }
 
 void init_slam(SLAM_attr *attr, Pos pos, PointCloud *lidarPointCloud)
@@ -356,7 +450,6 @@ void init_slam(SLAM_attr *attr, Pos pos, PointCloud *lidarPointCloud)
     slam_state *s = state_for(attr);
     attr->frameCount = 0;
     attr->error = 0.0;
-    memset(s->roots, 0, sizeof(s->roots)); /* attr may be fresh stack memory */
     map_frame(attr, s, pos, lidarPointCloud, 0);
     attr->frameCount++;
 }
@@ -387,6 +480,7 @@ static Pos localization_fast(SLAM_attr *attr, slam_state *s, double transform[6]
                             ROWS, COLS, NULL, s->d_sums));
     CK(navgpu_download(c, s->h_sums, s->d_sums, sizeof(s->h_sums)));
     CK(navgpu_sync(c));
+    PROF_ADD(2, s->prof_t0);
     /* merge the rows' (count, mean, centred M2) with Chan et al.'s pairwise
      * update: M2 = M2a + M2b + |mb - ma|^2 na nb / (na + nb) */
     double mean[3] = {0.0, 0.0, 0.0}, M2 = 0.0, n = 0.0, nq = 0.0;
@@ -476,6 +570,7 @@ Pos slam_localization(SLAM_attr *attr, PointCloud *lidarPointCloud,
     transform[5] = pos_predict.yaw - pos_last.yaw;
     double t[3] = {pos_predict.x, pos_predict.y, pos_predict.z};
 
+    s->prof_t0 = prof_on() ? now_s() : 0.0;
     /* GPU: transform, features, per-row 1-NN (src/slam.c:185-244) */
     CK(navgpu_upload(c, s->d_lidar, &lidarPointCloud->ToF_position[0][0],
                      24 * NPTS));
@@ -511,6 +606,8 @@ Pos slam_localization(SLAM_attr *attr, PointCloud *lidarPointCloud,
     if (CPcount > 0)
         CK(navgpu_download(c, result, s->d_list, sizeof(NeighborResult) * (size_t)CPcount));
     CK(navgpu_sync(c));
+    PROF_ADD(2, s->prof_t0);
+    const double pt1 = prof_on() ? now_s() : 0.0;
 
     /* host: Adam on the translation (src/slam.c:218-379) */
     double learningRate = 0.1, tolerance = 1e-6;
@@ -561,6 +658,7 @@ Pos slam_localization(SLAM_attr *attr, PointCloud *lidarPointCloud,
     g_last_queries = nqueries;
     g_last_cp = CPcount;
     g_last_iters = iter; /* the iteration that converged, or 200 */
+    PROF_ADD(3, pt1);
     if (validGradientCount > 0)
         attr->error = sqrt(totalError / validGradientCount);
     else

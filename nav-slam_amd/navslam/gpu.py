@@ -62,6 +62,10 @@ def _declare(L):
         "navgpu_kd_build_host": (C.c_int, [_vp, _vp, _sz, C.c_int]),
         "navgpu_malloc": (C.c_int, [_vp, _sz, C.POINTER(_vp)]),
         "navgpu_free": (None, [_vp, _vp]),
+        "navgpu_host_alloc": (C.c_int, [_vp, _sz, C.POINTER(_vp)]),
+        "navgpu_host_free": (None, [_vp, _vp]),
+        "navgpu_kd_rows_nodes_dev": (C.c_int, [_vp, _vp, _vp, C.c_int, C.c_int, C.c_uint64,
+                                               _vp, _vp]),
         "navgpu_upload": (C.c_int, [_vp, _vp, _vp, _sz]),
         "navgpu_download": (C.c_int, [_vp, _vp, _vp, _sz]),
         "navgpu_side_mark": (C.c_int, [_vp]),
@@ -246,6 +250,11 @@ class NavGpu:
         self._check(self.L.navgpu_kd_build_rows_dev(
             self.h, _ptr(feat_src), _ptr(coords), R, Cc, _ptr(tree_pts), _ptr(tree_col),
             _ptr(tree_n), _ptr(mask)), "kd_build_rows_dev")
+
+    def kd_rows_nodes_dev(self, tree_pts, tree_n, R, Cc, host_base, nodes, row_off):
+        self._check(self.L.navgpu_kd_rows_nodes_dev(
+            self.h, _ptr(tree_pts), _ptr(tree_n), R, Cc, int(host_base), _ptr(nodes),
+            _ptr(row_off)), "kd_rows_nodes_dev")
 
     def kd_query_rows_dev(self, tree_pts, tree_n, feat_src, queries, R, Cc, nn_pos,
                           nn_dist, mask=None):

@@ -659,6 +659,50 @@ def test_rows_corr_matches_reference_dedup(gpu, orc, integer_mm):
     assert ek.sum() > 0 and (ek.sum() < (pos.cpu().numpy() >= 0).sum() or not integer_mm)
 
 
+@pytest.mark.parametrize("R,Cc", [(24, 640), (2100, 42)])
+def test_kd_rows_nodes_image_links_the_implicit_trees(gpu, R, Cc):
+    """navgpu_kd_rows_nodes_dev: the KDNode image (utils/kdtree.h:7-11) of the
+    row trees, with host addresses, links exactly the implicit layout of
+    buildKDTree (node of [lo,hi) at lo+(hi-lo)/2, utils/kdtree.c:65-82); rows
+    with no features give no nodes; 2100 rows take the offset scan past one
+    row per thread."""
+    import torch
+    from navslam.synth import l9_pair
+    _, tgt = l9_pair(R, Cc, seed=31)
+    tgt[1] = 0.0  # a flat row: no features, an empty tree
+    dev = torch.device("cuda", 0)
+    ts = torch.from_numpy(tgt).to(dev)
+    tree = torch.empty_like(ts)
+    tcol = torch.empty((R, Cc), dtype=torch.int32, device=dev)
+    tn = torch.empty(R, dtype=torch.int32, device=dev)
+    off = torch.full((R + 1,), -1, dtype=torch.int32, device=dev)
+    nodes = torch.empty((R * Cc, 5), dtype=torch.float64, device=dev)
+    host = np.zeros((R * Cc, 5), np.float64)
+    base = host.ctypes.data
+    torch.cuda.synchronize()
+    gpu.kd_build_rows_dev(ts, ts, R, Cc, tree, tcol, tn)
+    gpu.kd_rows_nodes_dev(tree, tn, R, Cc, base, nodes, off)
+    gpu.sync()
+    tn, off, tree = tn.cpu().numpy(), off.cpu().numpy(), tree.cpu().numpy()
+    assert tn[1] == 0 and (tn > 0).sum() > R // 2
+    _eq(off, np.concatenate([[0], np.cumsum(tn)]).astype(np.int32), "row offsets")
+    img = nodes.cpu().numpy()[: off[R]]
+    pts, links = img[:, :3], img[:, 3:].copy().view(np.uint64)
+    for r in range(R):
+        o, n = int(off[r]), int(tn[r])
+        _eq(pts[o:o + n], tree[r, :n], f"row {r} points")
+        want = np.zeros((n, 2), np.uint64)
+        stack = [(0, n)]
+        while stack:
+            lo, hi = stack.pop()
+            mid = lo + (hi - lo) // 2
+            for k, (a, b) in enumerate(((lo, mid), (mid + 1, hi))):
+                if a < b:
+                    want[mid, k] = base + 40 * (o + a + (b - a) // 2)
+                    stack.append((a, b))
+        _eq(links[o:o + n], want, f"row {r} links")
+
+
 @pytest.mark.parametrize("integer_mm", [False, True])
 def test_rows_corr_list_matches_reference_list(gpu, orc, integer_mm):
     """The exact mode's correspondence list built on the GPU
