@@ -46,6 +46,10 @@ namespace {
 
 constexpr int kWave = 64;
 constexpr int kRowsBlock = 512;     // 8 waves per row workgroup
+#ifndef NAVGPU_ROWS_BUILD_BLOCK
+#define NAVGPU_ROWS_BUILD_BLOCK 512
+#endif
+constexpr int kRowsBuildBlock = NAVGPU_ROWS_BUILD_BLOCK;  // k_rows_build (trees only)
 constexpr int kStackDepth = 14;     // implicit-tree height bound, n < 8192
 constexpr int kMaxRowCols = 8191;   // 13-bit stack-entry fields
 constexpr int kCurvTile = 256;
@@ -59,7 +63,10 @@ __device__ unsigned long long g_stamps[16];
   if ((threadIdx.x & 63) == 0) atomicAdd(&g_stamps[slot], (b) - (a))
 #define NV_STAMP_ADD0(slot, a, b) \
   if (threadIdx.x == 0) atomicAdd(&g_stamps[slot], (b) - (a))
+#define NV_COUNT0(slot) \
+  if (threadIdx.x == 0) atomicAdd(&g_stamps[slot], 1ull)
 #else
+#define NV_COUNT0(slot)
 #define NV_STAMP(v)
 #define NV_STAMP_ADD(slot, a, b)
 #define NV_STAMP_ADD0(slot, a, b)
@@ -234,6 +241,20 @@ __device__ int block_compact(int C, int *scratch, Flag flag, Write write) {
 // a chunk by pointer jumping over lanes (DESIGN.md §KD build). The final
 // layout is smalls | pivot | tape[S+1..m) with tape[S] moved to `last`.
 // ------------------------------------------------------------------------
+// Where the tape chain of a small position p leads (tape[x] = tape[x - L]
+// while x is small with L larges before it): every position of p's run of
+// smalls [s, p] has the same L = p - sp, so the chain jumps by multiples of L
+// to the first position below s. s = one past the last large below p in this
+// wave (lbelow = the wave's large ballot masked to lanes below p), else the
+// wave's first position (the run then continues into earlier positions,
+// still of the same L). One hop per run of smalls instead of one per L.
+__device__ __forceinline__ int tape_jump(int p, int sp, unsigned long long lbelow,
+                                         int wave_p0) {
+  const int k = p - sp;  // >= 1
+  const int s = lbelow ? wave_p0 + kWave - __clzll(lbelow) : wave_p0;
+  return p - k * ((p - s + k) / k);
+}
+
 template <class IdxT, bool GMEM = false>
 __device__ void wave_nth_element(const double *key, IdxT *P, IdxT *T,
                                  int first, int last, int nth, int lane) {
@@ -260,15 +281,17 @@ __device__ void wave_nth_element(const double *key, IdxT *P, IdxT *T,
         k_n = key[e_n];
       }
       const unsigned long long bal = __ballot(small);
+      const unsigned long long lbal = __ballot(act && !small);
       const int sp = S + lanes_below(bal);
       // tape value of position p: bit 31 = resolved, low bits = the value, or
       // (unresolved) the chunk lane whose value it equals
       unsigned w = 0x80000000u | (unsigned)e;
-      if (small) {
-        if (sp < cs)
-          w = 0x80000000u | (unsigned)T[first + sp];
-        else if (sp != p)
-          w = (unsigned)(sp - cs);
+      if (small && sp != p) {
+        const int y = tape_jump(p, sp, lbal & ((1ull << lane) - 1ull), cs);
+        if (y < cs)
+          w = 0x80000000u | (unsigned)T[first + y];
+        else
+          w = (unsigned)(y - cs);
       }
       // pointer jumping: one shuffle per round (taking the pointee's word is
       // right both when it is resolved and when it is a further pointer)
@@ -299,71 +322,102 @@ __device__ void wave_nth_element(const double *key, IdxT *P, IdxT *T,
 // The reference nth_element for ONE subarray by the whole block (the top of
 // the tree, where a single wave would leave the rest of the block idle): the
 // same tape rule as wave_nth_element, one block-wide chunk of blockDim
-// positions per step. Small counts are prefix-summed across the waves;
-// tape chains that cross waves are resolved by pointer jumping through LDS
-// (bit 31 = resolved, else the chunk position whose value it equals).
-// Requires blockDim.x <= kBlockNthMax; P/T in LDS, or in global memory
-// (k_kd_level: every chunk ends at a barrier, which orders the waves'
-// global writes at workgroup scope).
+// positions per step. Small counts are prefix-summed across the waves. Tape
+// chains are first followed inside each wave with shuffles (a pointer always
+// leads to a lower position, so what is left points into an earlier wave),
+// then across waves by pointer jumping through LDS, one barrier per round
+// (double-buffered words, a rotating any-unresolved flag); the common chunk
+// with no cross-wave chain costs two barriers. Requires blockDim.x <=
+// kBlockNthMax; P/T in LDS, or in global memory (k_kd_level: the barriers
+// order the waves' global writes at workgroup scope).
 constexpr int kBlockNthMax = 1024;
-template <class IdxT>
+#ifndef NAVGPU_BLOCK_TO_WAVE
+#define NAVGPU_BLOCK_TO_WAVE 256
+#endif
+// windows this short finish on wave 0 alone (a block pass costs ~4 barriers
+// whatever its length; a wave pass over a few 64-position chunks needs none)
+constexpr int kBlockToWave = NAVGPU_BLOCK_TO_WAVE;
+template <class IdxT, bool GMEM = false>
 __device__ void block_nth_element(const double *key, IdxT *P, IdxT *T, int first,
                                   int last, int nth) {
-  __shared__ unsigned bw[kBlockNthMax];
-  __shared__ int bcnt[kBlockNthMax / kWave + 1];
-  __shared__ int bflag;
+  __shared__ unsigned bw[2 * kBlockNthMax];
+  __shared__ int bcnt[2][kBlockNthMax / kWave];
+  __shared__ int bany[3];
   const int tid = threadIdx.x, lane = tid & (kWave - 1), wid = tid / kWave;
-  const int bd = blockDim.x, nw = bd / kWave;
+  const int bd = blockDim.x, nw = bd / kWave, wbase = wid * kWave;
+  if (tid < 3) bany[tid] = 0;
+  __syncthreads();
+  int rnd = 0, chunk = 0;  // running counters (buffer and flag rotation)
   while (first < last) {
+    if (last - first < kBlockToWave) {
+      if (wid == 0) wave_nth_element<IdxT, GMEM>(key, P, T, first, last, nth, lane);
+      if (GMEM) __threadfence_block();
+      __syncthreads();
+      return;
+    }
     const int pe = (int)P[last];
     const double pk = key[pe];
     const int m = last - first;
     int S = 0;
-    for (int cs = 0; cs < m; cs += bd) {
+    NV_COUNT0(13);
+    for (int cs = 0; cs < m; cs += bd, ++chunk) {
+      NV_COUNT0(14);
       const int p = cs + tid;
       const bool act = p < m;
       const int e = act ? (int)P[first + p] : 0;
       const bool small = act && ((key[e] - pk) <= 0.0);  // kdtree.c:31-43
       const unsigned long long bal = __ballot(small);
-      if (lane == 0) bcnt[wid] = __popcll(bal);
+      const unsigned long long lbal = __ballot(act && !small);
+      int *cnt = bcnt[chunk & 1];
+      if (lane == 0) cnt[wid] = __popcll(bal);
+      // also orders the previous chunk's T writes before this chunk's reads
       __syncthreads();
       int before = 0, tot = 0;
       for (int w = 0; w < nw; ++w) {
-        const int c = bcnt[w];
+        const int c = cnt[w];
         before += w < wid ? c : 0;
         tot += c;
       }
       const int sp = S + before + lanes_below(bal);
+      // bit 31 = resolved value, else the chunk position it equals
       unsigned w = 0x80000000u | (unsigned)e;
-      if (small) {
-        if (sp < cs)
-          w = 0x80000000u | (unsigned)T[first + sp];
-        else if (sp != p)
-          w = (unsigned)(sp - cs);
+      if (small && sp != p) {
+        const int y = tape_jump(p, sp, lbal & ((1ull << lane) - 1ull), cs + wbase);
+        if (y < cs)
+          w = 0x80000000u | (unsigned)T[first + y];
+        else
+          w = (unsigned)(y - cs);
       }
-      // block-wide pointer jumping
+      // inside the wave: shuffles, no barrier
       for (;;) {
-        bw[tid] = w;
-        if (tid == 0) bflag = 0;
+        const bool loc = !(w >> 31) && (int)w >= wbase;
+        if (!__ballot(loc)) break;
+        const unsigned o = __shfl(w, loc ? (int)w - wbase : lane, kWave);
+        if (loc) w = o;
+      }
+      // across waves: publish, barrier, follow; until no word is unresolved
+      for (;;) {
+        unsigned *cur = bw + (rnd & 1) * kBlockNthMax;
+        const int f = rnd % 3;
+        cur[tid] = w;
+        if (!(w >> 31)) bany[f] = 1;
+        if (tid == 0) bany[(rnd + 1) % 3] = 0;  // last read two rounds ago
         __syncthreads();
-        if (!(w >> 31)) {
-          w = bw[w & (kBlockNthMax - 1)];
-          if (!(w >> 31)) bflag = 1;
-        }
-        __syncthreads();
-        if (!bflag) break;
-        __syncthreads();  // everyone has read bflag before it is reset
+        const bool more = bany[f] != 0;
+        ++rnd;
+        if (!more) break;
+        NV_COUNT0(15);
+        if (!(w >> 31)) w = cur[w & (kBlockNthMax - 1)];
       }
       if (act) T[first + p] = (IdxT)(w & 0x7fffffffu);
       if (small) P[first + sp] = (IdxT)e;
       S += tot;
-      __syncthreads();  // this chunk's T before the next chunk reads it
     }
+    __syncthreads();  // the last chunk's T and P before the tape copy
     for (int q = S + tid; q < m; q += bd) {
       const int v = (int)T[first + q];
       P[q == S ? last : first + q] = (IdxT)v;
     }
-    __syncthreads();
     if (tid == 0) P[first + S] = (IdxT)pe;
     __syncthreads();
     const int i = first + S;
@@ -1263,7 +1317,7 @@ __global__ __launch_bounds__(NT) void k_rows_screen(
 }
 
 // ------------------------------------------- split per-row build / query
-__global__ __launch_bounds__(kRowsBlock) void k_rows_build(
+__global__ __launch_bounds__(kRowsBuildBlock) void k_rows_build(
     const double *__restrict__ feat_src, const double *__restrict__ coords,
     int R, int C, double *__restrict__ tree_pts, int32_t *__restrict__ tree_col,
     int32_t *__restrict__ tree_n, int32_t *__restrict__ mask_out) {
@@ -1842,7 +1896,7 @@ __global__ __launch_bounds__(1024) void k_kd_level(const double *__restrict__ FC
   const double *key = FC + (size_t)((depth0 + d) % 3) * n;
   // the block-wide tape pass on global P/T: 1024 positions per step (the
   // barriers order the waves' global writes at workgroup scope)
-  block_nth_element<uint32_t>(key, P, T, lo, hi - 1, lo + (hi - lo) / 2);
+  block_nth_element<uint32_t, true>(key, P, T, lo, hi - 1, lo + (hi - lo) / 2);
 }
 
 __global__ __launch_bounds__(1024) void k_kd_leaves(double *__restrict__ pts,
@@ -3497,7 +3551,7 @@ struct TimedRegion {
 // dynamic LDS a tree-building kernel may request: the device limit minus
 // the static LDS of block_nth_element (pointer-jumping words + counts)
 int lds_limit() {
-  constexpr int kStaticLds = 4 * kBlockNthMax + 4 * (kBlockNthMax / kWave + 2) + 256;
+  constexpr int kStaticLds = 8 * kBlockNthMax + 8 * (kBlockNthMax / kWave) + 16 + 256;
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) return 65536 - kStaticLds;
   int v = 0;
@@ -3877,7 +3931,7 @@ int navgpu_kd_build_rows_dev(navgpu_ctx *ctx, const double *feat_src,
   const RowsLds L = rows_lds(C, kRowsBlock, false);
   RC(set_lds(k_rows_build, L.total));
   TimedRegion tr(ctx, "rows_build");
-  hipLaunchKernelGGL(k_rows_build, dim3(R), dim3(kRowsBlock), L.total,
+  hipLaunchKernelGGL(k_rows_build, dim3(R), dim3(kRowsBuildBlock), L.total,
                      ctx->stream, feat_src, coords, R, C, tree_pts, tree_col,
                      tree_n, mask_out);
   CHECK_LAUNCH("k_rows_build");
