@@ -83,6 +83,8 @@ def parse():
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_k3.json"),
                    help="per-step HBM bytes measured by scripts/round_profile.sh (PMC passes)")
     p.add_argument("--no-traffic-json", action="store_true")
+    p.add_argument("--no-stream-copy", action="store_true",
+                   help="skip the STREAM-copy ceiling measurement")
     p.add_argument("--json-out", default=None)
     return p.parse_args()
 
@@ -513,6 +515,7 @@ def main():
         gather_buf = None
         if a.workload == "k4" and ws > 1:
             gather_buf = torch.empty(ws * packed.numel(), dtype=torch.uint8, device=dev)
+        do_gather = [True]  # scans/s are also reported without the gather
 
         def step():
             if a.workload == "k4":  # one launch over the rank's whole batch
@@ -520,7 +523,7 @@ def main():
                     g.rows_match_batch_dev(bsrc, btgt, pairs, R, Cc, sm, tm, idx, dst)
             else:
                 g.rows_match_dev(srcs[0], tgts[0], R, Cc, sm[0], tm[0], idx[0], dst[0])
-            if gather_buf is not None:
+            if gather_buf is not None and do_gather[0]:
                 shard.gather_matches(packed, gather_buf)
         # matches = feature queries actually searched (constant per pair)
         step()
@@ -601,6 +604,45 @@ def main():
         torch.cuda.synchronize()
         kt_iso = timing_collect()
     timing_on(False)
+    # K4 on N > 1 ranks: the same steps again without the all-gather
+    no_gather = None
+    if a.workload in ("k2", "k4") and gather_buf is not None:
+        do_gather[0] = False
+        torch.cuda.synchronize()
+        dist.barrier()
+        t2 = time.perf_counter()
+        for _ in range(a.steps):
+            step()
+        torch.cuda.synchronize()
+        dist.barrier()
+        el2 = shard.max_over_ranks(time.perf_counter() - t2, dev)
+        do_gather[0] = True
+        no_gather = {"value": round(job_matches * a.steps / el2, 1),
+                     "ms_per_step": round(1000.0 * el2 / a.steps, 4),
+                     "gather_bytes_per_rank": int(ws * packed.numel())}
+    # measured HBM ceiling: a STREAM copy of 1 GiB, far above the
+    # 256 MiB Infinity Cache, on the library's stream (read + write bytes)
+    stream_copy = None
+    if rank == 0 and not a.no_stream_copy:
+        nb = 1 << 30
+        sbuf = torch.empty(nb, dtype=torch.uint8, device=dev)
+        dbuf = torch.empty(nb, dtype=torch.uint8, device=dev)
+        sbuf.fill_(1)
+        for _ in range(3):
+            g.stream_copy_dev(dbuf, sbuf, nb)
+        torch.cuda.synchronize()
+        g.timing(True)
+        g.timing_read("stream_copy", reset=True)
+        for _ in range(10):
+            g.stream_copy_dev(dbuf, sbuf, nb)
+        torch.cuda.synchronize()
+        ms, n = g.timing_read("stream_copy", reset=True)
+        g.timing(False)
+        if n:
+            stream_copy = {"GBs": round(2 * nb / (ms / n * 1e-3) / 1e9, 1),
+                           "bytes_per_copy": 2 * nb, "copies": n,
+                           "kernel": "k_stream_copy (16-B loads/stores, 1 GiB -> 1 GiB)"}
+        del sbuf, dbuf
 
     out = None
     if rank == 0:
@@ -650,6 +692,10 @@ def main():
                                     "(SURVEY 8d)"),
                     "note": ("f64 VALU-bound screen (chunk-box pruned scan); rows with a tie "
                              "add the latency-bound Lomuto tree build (DESIGN.md)")}
+        if roof is not None and stream_copy is not None:
+            roof["stream_copy"] = stream_copy
+            if roof.get("achieved"):
+                roof["frac_of_stream_copy"] = round(roof["achieved"] / stream_copy["GBs"], 4)
         path = None
         if path_bytes is not None:
             def path_of(tab, label):
@@ -686,6 +732,8 @@ def main():
                                       {k: round(1000.0 * v[0] / max(v[1], 1), 2)
                                        for k, v in kt_iso.items()}),
                "cpu_baseline": cpu}
+        if no_gather is not None:
+            out["without_gather"] = no_gather
         line = json.dumps(out)
         print(line, flush=True)
         if a.json_out:

@@ -225,6 +225,12 @@ int navgpu_upload(navgpu_ctx *ctx, void *dst_dev, const void *src_host,
                   size_t bytes);
 int navgpu_download(navgpu_ctx *ctx, void *dst_host, const void *src_dev,
                     size_t bytes);
+/* Measured HBM ceiling for the roofline: a device-to-device copy
+ * of `bytes` (a multiple of 16, both pointers 16-B aligned) by a plain
+ * streaming kernel on the context's stream, timed as "stream_copy". Not part
+ * of the reference interface. */
+int navgpu_stream_copy_dev(navgpu_ctx *ctx, void *dst_dev, const void *src_dev,
+                           size_t bytes);
 
 /* Copies that overlap later work: navgpu_side_mark records the current
  * point of the context's stream; navgpu_side_download copies device->host on

@@ -4609,3 +4609,47 @@ int navgpu_pair_knn_dev(navgpu_ctx *ctx, const double *src, const double *tgt,
 }
 
 }  // extern "C"
+
+// ---- measured HBM ceiling (a STREAM-copy figure beside the 8 TB/s
+// peak). 16-B loads and stores, kStreamU vectors per lane with all loads
+// issued before any store; blocks dealt round-robin over the XCDs like every
+// other launch, each taking a contiguous span so a wave streams whole lines.
+namespace {
+constexpr int kStreamU = 8;
+__global__ __launch_bounds__(256) void k_stream_copy(const int4 *__restrict__ src,
+                                                     int4 *__restrict__ dst, size_t n) {
+  const size_t per = (size_t)kStreamU * blockDim.x;
+  for (size_t b = (size_t)blockIdx.x * per; b < n; b += (size_t)gridDim.x * per) {
+    int4 v[kStreamU];
+#pragma unroll
+    for (int u = 0; u < kStreamU; ++u) {
+      const size_t i = b + (size_t)u * blockDim.x + threadIdx.x;
+      if (i < n) v[u] = src[i];
+    }
+#pragma unroll
+    for (int u = 0; u < kStreamU; ++u) {
+      const size_t i = b + (size_t)u * blockDim.x + threadIdx.x;
+      if (i < n) dst[i] = v[u];
+    }
+  }
+}
+}  // namespace
+
+extern "C" {
+
+int navgpu_stream_copy_dev(navgpu_ctx *ctx, void *dst, const void *src, size_t bytes) {
+  ARG_CHECK(ctx);
+  if (!bytes) return NAVGPU_OK;
+  ARG_CHECK(dst && src && bytes % 16 == 0 && (uintptr_t)dst % 16 == 0 &&
+            (uintptr_t)src % 16 == 0);
+  const size_t n = bytes / 16;
+  const size_t per = (size_t)kStreamU * 256;
+  const unsigned nb = (unsigned)std::max<size_t>(1, std::min<size_t>(8192, (n + per - 1) / per));
+  TimedRegion tr(ctx, "stream_copy");
+  hipLaunchKernelGGL(k_stream_copy, dim3(nb), dim3(256), 0, ctx->stream, (const int4 *)src,
+                     (int4 *)dst, n);
+  CHECK_LAUNCH("k_stream_copy");
+  return NAVGPU_OK;
+}
+
+}  // extern "C"

@@ -68,6 +68,7 @@ def _declare(L):
                                                _vp, _vp]),
         "navgpu_upload": (C.c_int, [_vp, _vp, _vp, _sz]),
         "navgpu_download": (C.c_int, [_vp, _vp, _vp, _sz]),
+        "navgpu_stream_copy_dev": (C.c_int, [_vp, _vp, _vp, _sz]),
         "navgpu_side_mark": (C.c_int, [_vp]),
         "navgpu_side_download": (C.c_int, [_vp, _vp, _vp, _sz]),
         "navgpu_timing_enable": (None, [_vp, C.c_int]),
@@ -161,6 +162,12 @@ class NavGpu:
 
     def timing(self, on=True):
         self.L.navgpu_timing_enable(self.h, 1 if on else 0)
+
+    def stream_copy_dev(self, dst, src, nbytes):
+        """Device-to-device copy by a plain streaming kernel (the measured HBM
+        ceiling beside the roofline's peak; timed as "stream_copy")."""
+        self._check(self.L.navgpu_stream_copy_dev(self.h, _ptr(dst), _ptr(src), nbytes),
+                    "stream_copy_dev")
 
     def knn_fallbacks(self):
         """Queries of the last knn call that took the exact slow path (-1 if

@@ -869,3 +869,18 @@ def test_shim_kdtree_api_matches_reference_golden(golden):
                 assert bd.value == nnd[i]
                 _eq(np.array([res.x, res.y, res.z]), nn[i], "nearest")
         sh.L.freeKDTree(root)
+
+
+# ------------------------------------------------- measured HBM ceiling
+def test_stream_copy_copies_every_byte(gpu):
+    """navgpu_stream_copy_dev (the bench's STREAM-copy ceiling) moves the
+    buffer exactly, including a tail that is not a whole block's span."""
+    import torch
+    dev = torch.device("cuda", 0)
+    n = (1 << 20) * 16 + 16 * 37
+    src = torch.randint(0, 256, (n,), dtype=torch.uint8, device=dev)
+    dst = torch.zeros(n + 16, dtype=torch.uint8, device=dev)
+    gpu.stream_copy_dev(dst, src, n)
+    torch.cuda.synchronize()
+    assert torch.equal(dst[:n], src)
+    assert int(dst[n:].sum()) == 0
