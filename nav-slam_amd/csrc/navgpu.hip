@@ -2175,6 +2175,7 @@ __global__ __launch_bounds__(256) void k_bbox_partial(const double *__restrict__
   __shared__ double s[4][6];
   double v6[6] = {INFINITY, INFINITY, INFINITY, -INFINITY, -INFINITY, -INFINITY};
   // batches of 4 points per thread, all loads of a batch in flight together
+  // (flat 16-B loads of the 3n doubles measured the same, r2)
   constexpr int U = 4;
   const size_t stride = (size_t)gridDim.x * blockDim.x;
   for (size_t ib = (size_t)blockIdx.x * blockDim.x + threadIdx.x; ib < n; ib += U * stride) {
@@ -2411,9 +2412,11 @@ __device__ __forceinline__ int bin_side(const BinJob &J, int &blk) {
 }
 
 #ifndef NAVGPU_BIN_UNROLL
-#define NAVGPU_BIN_UNROLL 8
+#define NAVGPU_BIN_UNROLL 16
 #endif
-constexpr int kBinUnroll = NAVGPU_BIN_UNROLL;  // points per thread with loads in flight
+// points per thread with loads in flight (r2 sweep: 4 / 8 / 16 -> build 97 /
+// 98 / 96 us; the k_bin_* blocks take 4096 points, so 16 is one batch)
+constexpr int kBinUnroll = NAVGPU_BIN_UNROLL;
 
 struct P3 {
   double x, y, z;
@@ -2484,6 +2487,9 @@ __global__ __launch_bounds__(256) void k_bin_scatter(BinJob J,
   });
 }
 
+#ifndef NAVGPU_BIN_P
+#define NAVGPU_BIN_P 4096  // minimum points per k_bin_hist / k_bin_scatter block
+#endif
 #ifndef NAVGPU_BIN_FINE_THREADS
 #define NAVGPU_BIN_FINE_THREADS 512
 #endif
@@ -4418,7 +4424,7 @@ static int knn_run(navgpu_ctx *ctx, const double *tgt, size_t nt, const double *
   for (int side = 0; side < 2; ++side) {
     BinSide &S = J.s[side];
     S.n = (int)ns[side];
-    S.P = (int)std::max<size_t>(4096, (ns[side] / 2000 + 256) / 256 * 256);
+    S.P = (int)std::max<size_t>(NAVGPU_BIN_P, (ns[side] / 2000 + 256) / 256 * 256);
     S.nblk = (int)std::max<size_t>(1, (ns[side] + S.P - 1) / S.P);
     S.tab = (int)ntab;
     S.sub = side ? (int)nt : 0;
