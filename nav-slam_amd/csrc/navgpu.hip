@@ -2976,10 +2976,14 @@ __device__ __forceinline__ void knn_one(
 #endif
   } else {
     // K listed points have dsq <= dk2: a valid starting bound for the slow
-    // path, which runs in its own launch (k_knn_slow)
+    // path, which runs in its own launch (k_knn_slow). Not after an overfull
+    // run: its keys' offsets wrapped, so two slots can decode to the same
+    // record and the list may hold fewer than K distinct points (a bound
+    // from it can exclude a true neighbour); the slow path then starts from
+    // an infinite bound (the ring search).
     const int e = atomicAdd(L_.n_slow, 1);
     L_.slow_q[e] = (int)q;
-    L_.slow_thr[e] = dk < INFINITY ? dk2 * (1.0 + 0x1p-46) : INFINITY;
+    L_.slow_thr[e] = (dk < INFINITY && !overflow) ? dk2 * (1.0 + 0x1p-46) : INFINITY;
   }
   NV_STAMP(ts2);
   NV_STAMP_ADD(4, ts1, ts2);

@@ -421,6 +421,23 @@ def test_knn_k3_full_size_all_queries(gpu, orc):
     _eq(gd[s], bd, "sampled dist vs brute force")
 
 
+@pytest.mark.parametrize("integer_mm", [False, True])
+def test_knn_global_on_l9_scan(gpu, orc, integer_mm):
+    """Global mode on a lidar-shaped pair instead of the uniform K3 cloud:
+    points on surfaces (most grid cells empty, the rest dense), 2 % dropouts
+    that all sit at (0, 0, 0) (utils/pointcloud.c:24-27: one cell holding
+    thousands of identical points, so LDS-overflow tiles, overfull runs and
+    the slow path with massive distance ties), and integer-mm coordinates.
+    Every query against the oracle's exact grid k-NN."""
+    from navslam.synth import l9_pair
+    src, tgt = l9_pair(128, 2048, seed=21, integer_mm=integer_mm)
+    for k in (1, 8):
+        gi, gd = gpu.knn(tgt, src, k)
+        ri, rd = orc.knn_grid(tgt, src, k)
+        _eq(gi, ri, f"l9 integer_mm={integer_mm} k={k}: idx")
+        _eq(gd, rd, f"l9 integer_mm={integer_mm} k={k}: dist")
+
+
 def _digest_inputs_match(dg, prefix, src, tgt):
     from golden.make_golden import sha
     if sha(src) != str(dg[prefix + "_src"]) or sha(tgt) != str(dg[prefix + "_tgt"]):
