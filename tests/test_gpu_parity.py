@@ -438,6 +438,35 @@ def test_knn_global_on_l9_scan(gpu, orc, integer_mm):
         _eq(gd, rd, f"l9 integer_mm={integer_mm} k={k}: dist")
 
 
+def _degenerate_clouds(name, rng):
+    n = 200_000
+    if name == "line":  # one grid axis at its 2048-cell cap, the others 1 cell
+        t = np.c_[rng.uniform(0, 1e4, n), rng.normal(0, 1e-3, n), np.zeros(n)]
+        q = np.c_[rng.uniform(-10, 1e4 + 10, 50_000), rng.normal(0, 1, 50_000),
+                  rng.normal(0, 1, 50_000)]
+    elif name == "plane":  # a flat target, queries above and below it
+        t = np.c_[rng.uniform(0, 1e3, n), rng.uniform(0, 1e3, n), np.zeros(n)]
+        q = np.c_[rng.uniform(0, 1e3, 50_000), rng.uniform(0, 1e3, 50_000),
+                  rng.normal(0, 5, 50_000)]
+    else:  # two dense clusters 1e6 mm apart: almost every cell empty
+        t = np.concatenate([rng.normal(0, 10, (n // 2, 3)), rng.normal(1e6, 10, (n // 2, 3))])
+        q = np.concatenate([rng.normal(0, 12, (25_000, 3)), rng.normal(1e6, 12, (25_000, 3)),
+                            rng.uniform(0, 1e6, (1_000, 3))])
+    return t, q
+
+
+@pytest.mark.parametrize("name", ["line", "plane", "far_clusters"])
+def test_knn_global_degenerate_distributions(gpu, orc, name):
+    """Distributions the uniform grid handles worst (overflow tiles, overfull
+    runs, a slow path for most queries, rings across empty space): every
+    query against the oracle's exact grid k-NN, k = 8."""
+    t, q = _degenerate_clouds(name, np.random.default_rng(5))
+    gi, gd = gpu.knn(t, q, 8)
+    ri, rd = orc.knn_grid(t, q, 8)
+    _eq(gi, ri, f"{name}: idx")
+    _eq(gd, rd, f"{name}: dist")
+
+
 def _digest_inputs_match(dg, prefix, src, tgt):
     from golden.make_golden import sha
     if sha(src) != str(dg[prefix + "_src"]) or sha(tgt) != str(dg[prefix + "_tgt"]):
