@@ -254,6 +254,30 @@ def test_rows_match_edge_cases(gpu, orc):
         _eq(gpu.rows_match(c, t)[3], orc.rows_match(c, t)[3], f"dist {c.shape}")
 
 
+def test_rows_match_nonfinite_and_dense_features(gpu, orc):
+    """Per-row mode on inputs the L9 generator never makes: non-finite
+    coordinates (NaN / +-inf never pass the curvature test and never win a
+    distance comparison in the reference; utils/kdtree.c:117, src/slam.c:11-61)
+    and zig-zag rows where almost every point is a feature (the widest trees
+    and the longest Lomuto chains per row)."""
+    from navslam.synth import l9_pair
+    rng = np.random.default_rng(31)
+    src, tgt = l9_pair(32, 512, seed=4)
+    for a in (src, tgt):
+        for v in (np.nan, np.inf, -np.inf):
+            r, c, ax = rng.integers(0, 32, 60), rng.integers(0, 512, 60), rng.integers(0, 3, 60)
+            a[r, c, ax] = v
+    zz = np.zeros((8, 1024, 3))
+    zz[..., 0] = np.arange(1024)[None, :] * 10.0
+    zz[..., 1] = np.where(np.arange(1024) % 2, 50.0, -50.0)[None, :] + rng.normal(0, 1, (8, 1024))
+    zz[..., 2] = np.arange(8)[:, None] * 100.0
+    for s_, t_, name in ((src, tgt, "non-finite"), (zz, zz[:, ::-1].copy() + 3.0, "zig-zag")):
+        got = gpu.rows_match(s_, t_)
+        ref = orc.rows_match(s_, t_)
+        for a, b, what in zip(got, ref, ("src_mask", "tgt_mask", "nn_idx", "nn_dist")):
+            _eq(a, b, f"{name}: {what}")
+
+
 def test_rows_screen_vs_tree_path(gpu, orc, monkeypatch):
     """The screened per-row path (exact argmin, the reference tree only for
     rows with a tie) == the tree on every row (NAVGPU_ROWS_SCREEN=0) == the
