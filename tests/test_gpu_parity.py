@@ -128,6 +128,23 @@ def test_kd_build_adversarial_orders(gpu, orc):
     _eq(gpu.kd_build(s), ts, "x-sorted input")
 
 
+@pytest.mark.parametrize("n", [3000, 100_000])
+def test_kd_build_nonfinite_and_signed_zeros(gpu, orc, n):
+    """buildKDTree's Lomuto compares (utils/kdtree.c:20-45) on NaN, +-inf and
+    -0.0 / +0.0 coordinates, in one workgroup's LDS (3000) and through the
+    grid-wide passes (100k). Compared bit for bit (uint64 view), so a -0.0
+    landing where the reference puts a +0.0 is caught."""
+    rng = np.random.default_rng(n + 7)
+    pts = np.round(rng.uniform(-20, 20, (n, 3)))
+    m = n // 50
+    for v in (np.nan, np.inf, -np.inf, -0.0, 0.0):
+        pts[rng.integers(0, n, m), rng.integers(0, 3, m)] = v
+    t, _ = orc.kd_build(pts.copy())
+    got = gpu.kd_build(pts)
+    np.testing.assert_array_equal(np.asarray(got).view(np.uint64), t.view(np.uint64),
+                                  err_msg=f"n={n}")
+
+
 def test_kd_build_level_parallel_equals_single_workgroup(gpu, monkeypatch):
     rng = np.random.default_rng(9)
     pts = np.round(rng.uniform(0, 300, (40000, 3)))
