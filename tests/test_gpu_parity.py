@@ -971,3 +971,41 @@ def test_stream_copy_copies_every_byte(gpu):
     torch.cuda.synchronize()
     assert torch.equal(dst[:n], src)
     assert int(dst[n:].sum()) == 0
+
+
+def test_two_contexts_in_flight_match_one_at_a_time():
+    """bench.py's K3 step keeps two pairs in flight on two contexts (own
+    stream, workspace and outputs each). Their results must equal those of
+    the same pairs run one at a time: no state is shared between contexts."""
+    import torch
+    from navslam.gpu import NavGpu
+    from navslam.synth import uniform_pair
+    dev = torch.device("cuda", 0)
+    R, Cc, k = 128, 1024, 8
+    N = R * Cc
+    pairs = [tuple(torch.from_numpy(a).to(dev) for a in uniform_pair(R, Cc, seed_src=50 + j,
+                                                                     seed_tgt=60 + j))
+             for j in range(4)]
+    streams = [torch.cuda.Stream(dev) for _ in range(2)]
+    ctxs = [NavGpu(0, s.cuda_stream) for s in streams]
+
+    def outs():
+        return (torch.empty((R, Cc), dtype=torch.int32, device=dev),
+                torch.empty((R, Cc), dtype=torch.int32, device=dev),
+                torch.empty((N, k), dtype=torch.int32, device=dev),
+                torch.empty((N, k), dtype=torch.float64, device=dev))
+    ref = []
+    for s, t in pairs:  # one at a time
+        o = outs()
+        ctxs[0].pair_knn_dev(s, t, R, Cc, k, *o)
+        torch.cuda.synchronize()
+        ref.append([x.cpu().numpy() for x in o])
+    got = [outs() for _ in pairs]
+    for j, (s, t) in enumerate(pairs):  # two in flight
+        ctxs[j % 2].pair_knn_dev(s, t, R, Cc, k, *got[j])
+    torch.cuda.synchronize()
+    for j in range(len(pairs)):
+        for a, b, what in zip(got[j], ref[j], ("src_mask", "tgt_mask", "idx", "dist")):
+            _eq(a.cpu().numpy(), b, f"pair {j} {what}")
+    for c in ctxs:
+        c.close()
