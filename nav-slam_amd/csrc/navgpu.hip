@@ -2412,10 +2412,11 @@ __device__ __forceinline__ int bin_side(const BinJob &J, int &blk) {
 }
 
 #ifndef NAVGPU_BIN_UNROLL
-#define NAVGPU_BIN_UNROLL 16
+#define NAVGPU_BIN_UNROLL 8
 #endif
-// points per thread with loads in flight (r2 sweep: 4 / 8 / 16 -> build 97 /
-// 98 / 96 us; the k_bin_* blocks take 4096 points, so 16 is one batch)
+// points per thread with loads in flight (r2 sweep: 4 / 8 / 16 -> isolated
+// build 97 / 98 / 96 us, but the two-in-flight bench step 0.2805 ms with 16
+// against 0.2767 with 8: the build shares the chip with a query stage there)
 constexpr int kBinUnroll = NAVGPU_BIN_UNROLL;
 
 struct P3 {

@@ -12,7 +12,8 @@ import numpy as np
 
 PKG = os.path.dirname(os.path.abspath(__file__))
 LIBDIR = os.path.abspath(os.path.join(PKG, "..", "lib"))
-LIBNAVGPU = os.path.join(LIBDIR, "libnavgpu.so")
+# NAVGPU_LIB: an experimental build of the same library (A/B runs only)
+LIBNAVGPU = os.environ.get("NAVGPU_LIB") or os.path.join(LIBDIR, "libnavgpu.so")
 
 NAVGPU_OK = 0
 
