@@ -2495,7 +2495,10 @@ __global__ __launch_bounds__(256) void k_bin_scatter(BinJob J,
 #define NAVGPU_BIN_FINE_THREADS 512
 #endif
 #ifndef NAVGPU_BIN_MIN_SHIFT
-#define NAVGPU_BIN_MIN_SHIFT 9
+// coarse buckets of 2^10 cells (r2 two-in-flight bench A/B, two sessions of
+// 3 interleaved runs: 9 -> 0.2745 / 0.2744 ms, 10 -> 0.2716 / 0.2733, 11 ->
+// 0.2942; profiles/r2/bench_ab_r2l.txt)
+#define NAVGPU_BIN_MIN_SHIFT 10
 #endif
 constexpr int kBinFineThreads = NAVGPU_BIN_FINE_THREADS;
 
