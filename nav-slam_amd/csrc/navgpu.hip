@@ -2800,7 +2800,10 @@ __device__ __forceinline__ void knn_one(
     if (np > 2) {
       const auto last = cursor(ta + 2 * (np - 1));
       uint32_t v2 = 2;
-#pragma unroll 1
+#ifndef NAVGPU_KNN_UNROLL
+#define NAVGPU_KNN_UNROLL 1
+#endif
+#pragma unroll NAVGPU_KNN_UNROLL
       do {
         const f2 d = dist2(cur.load());
         const uint32_t lid = rid | (v2 & kOffMask);
