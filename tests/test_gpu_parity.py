@@ -1009,3 +1009,27 @@ def test_two_contexts_in_flight_match_one_at_a_time():
             _eq(a.cpu().numpy(), b, f"pair {j} {what}")
     for c in ctxs:
         c.close()
+
+
+def test_pair_knn_on_l9_scans_vs_oracle(gpu, orc):
+    """The bench's pair entry point (navgpu_pair_knn_dev: curvature of both
+    clouds on a side stream + global k-NN) on lidar-shaped scans: masks
+    against the oracle's extract_feature (src/slam.c:11-61) and every query
+    against its exact grid k-NN."""
+    import torch
+    from navslam.synth import l9_pair
+    dev = torch.device("cuda", 0)
+    R, Cc, k = 64, 2048, 8
+    src, tgt = l9_pair(R, Cc, seed=23)
+    s, t = torch.from_numpy(src).to(dev), torch.from_numpy(tgt).to(dev)
+    sm = torch.empty((R, Cc), dtype=torch.int32, device=dev)
+    tm = torch.empty((R, Cc), dtype=torch.int32, device=dev)
+    idx = torch.empty((R * Cc, k), dtype=torch.int32, device=dev)
+    dst = torch.empty((R * Cc, k), dtype=torch.float64, device=dev)
+    gpu.pair_knn_dev(s, t, R, Cc, k, sm, tm, idx, dst)
+    torch.cuda.synchronize()
+    _eq(sm.cpu().numpy(), orc.extract_feature(src), "src mask")
+    _eq(tm.cpu().numpy(), orc.extract_feature(tgt), "tgt mask")
+    ri, rd = orc.knn_grid(tgt, src, k)
+    _eq(idx.cpu().numpy(), ri, "idx")
+    _eq(dst.cpu().numpy(), rd, "dist")
