@@ -643,6 +643,8 @@ def main():
                            "bytes_per_copy": 2 * nb, "copies": n,
                            "kernel": "k_stream_copy (16-B loads/stores, 1 GiB -> 1 GiB)"}
         del sbuf, dbuf
+    if ws > 1:
+        dist.barrier()  # every rank leaves together (rank 0 ran the copy alone)
 
     out = None
     if rank == 0:
