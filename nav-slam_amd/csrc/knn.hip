@@ -1,0 +1,1434 @@
+// knn.hip — global-mode exact k-NN on MI355X (gfx950): the K3 configuration
+// (BASELINE.json configs[2]) and the batched global queries of the API.
+//
+// The reference has one nearest-neighbour search, per scan row over a KD tree
+// (utils/kdtree.c:110-152, driven from src/slam.c:236-252). Global mode is its
+// generalisation to one index over a whole target cloud and k neighbours per
+// query, ordered by (distance, index); for k = 1 it returns the reference KD
+// answer whenever the nearest distance is unique. Distances are
+// the reference formula, sqrt((dx*dx + dy*dy) + dz*dz) in f64, bit for bit.
+//
+// Pipeline of one call (DESIGN.md §3-§4 has the HBM layout and the roofline
+// of each kernel):
+//   k_bbox_partial, k_grid_params   target bbox -> uniform grid (cells of
+//                                   h/sx x h x h, ~occ targets per h^3)
+//   k_bin_hist, k_scan_*, k_bin_scatter, k_bin_fine
+//                                   both clouds counting-sorted by cell
+//                                   (LDS atomics only), written as 32-B
+//                                   records (f64 point, index, x column)
+//   k_knn<K>                        tiles of one grid row: the 9 neighbouring
+//                                   row segments staged in LDS (column-major),
+//                                   one query per lane: packed-f32 screen,
+//                                   survivors filtered into an LDS list and a
+//                                   sorted top-(K+1), f64 exact stage, a
+//                                   certificate that the answer is exact
+//   k_knn_slow<K>                   the uncertified rest, one wave per query
+#include "navgpu_common.h"
+
+using namespace nv;
+
+namespace {
+
+// ============================================================ the grid
+// Cells are numbered x-fastest, so the cells x-sx..x+sx of one (y,z) row are
+// contiguous in the cell-sorted arrays.
+struct GridParams {
+  double o[3];            // origin = target bbox min
+  double e[3], inv_e[3];  // cell edge per axis: x h / sx, y and z h
+  double h;               // the coarse edge
+  double delta;           // slack on cell boxes (cell assignment is f64 arithmetic)
+  double emax;            // largest bbox extent
+  int g[3];
+  int ncells;
+  int sx;                 // x cells per h: a query's block is cells x-sx .. x+sx,
+                          // y-1 .. y+1, z-1 .. z+1 (the reach is >= h on every axis)
+  int tile_w;             // query cells (x) per k_knn tile
+  int clamped;            // some axis hit the 2048-cell cap: its boundary cells
+                          // hold points beyond their nominal box
+};
+
+// one point of a cell-sorted cloud: the caller's f64 coordinates, its index
+// in the caller's array and the x index of its grid cell (the f64 binning's)
+struct __align__(16) PRec {
+  double x, y, z;
+  int idx, cx;
+};
+
+// ---- k_knn tile geometry (LDS budget: 4 blocks of 192 threads per CU)
+constexpr int kTileThreads = 192;  // 3 waves: a ~145-query tile fills them
+constexpr int kTileRec = 1568;     // staged records per tile (16 B each)
+constexpr int kTilePairs = kTileRec / 2 + 2;  // two spare pairs: read-ahead
+constexpr int kZgOff = 4 * kTilePairs;        // floats from the XY plane to the ZG plane
+constexpr int kTileCols = 136;     // staged columns per tile + 1
+constexpr double kTileQueries = 150.0;  // target queries per tile
+// survivor lists (NAVGPU_KNN_LIST=1): keys below a threshold are appended to
+// a per-lane LDS list and inserted into the sorted K+1 in batches; off by
+// default (the list's LDS costs a block per CU, r3 A/B in DESIGN.md §4)
+#ifndef NAVGPU_KNN_LIST
+#define NAVGPU_KNN_LIST 0
+#endif
+constexpr bool kList = NAVGPU_KNN_LIST;
+constexpr int kListCap = 12;       // survivors a lane holds before a drain
+constexpr int kKeyBits = 8;        // local id in the low bits of a packed key
+constexpr uint32_t kKeyMask = (1u << kKeyBits) - 1;
+constexpr uint32_t kNoKey = 0xffffffffu;
+
+constexpr int kBBoxBlocks = 1024;
+
+// Timing-only ablations of k_knn (never in the product build: -DNAVGPU_ABL=...
+// in scripts/build_variants.sh); the results are wrong in such builds.
+#ifndef NAVGPU_ABL
+#define NAVGPU_ABL 0
+#endif
+constexpr int kAbl = NAVGPU_ABL;
+constexpr int kAblNoQuery = 1;  // staging and barriers only
+constexpr int kAblNoExact = 2;  // no f64 exact stage: keys decoded, one store per query
+
+// per-block min/max of the finite coordinates -> part[block][6]
+__global__ __launch_bounds__(256) void k_bbox_partial(const double *__restrict__ p,
+                                                      size_t n, double *__restrict__ part) {
+  __shared__ double s[4][6];
+  double v6[6] = {INFINITY, INFINITY, INFINITY, -INFINITY, -INFINITY, -INFINITY};
+  // batches of 4 points per thread, all loads of a batch in flight together
+  constexpr int U = 4;
+  const size_t stride = (size_t)gridDim.x * blockDim.x;
+  for (size_t ib = (size_t)blockIdx.x * blockDim.x + threadIdx.x; ib < n; ib += U * stride) {
+    double v[U][3];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const size_t i = ib + u * stride;
+#pragma unroll
+      for (int a = 0; a < 3; ++a) v[u][a] = i < n ? p[3 * i + a] : INFINITY;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int a = 0; a < 3; ++a)
+        if (fabs(v[u][a]) < INFINITY) {
+          v6[a] = fmin(v6[a], v[u][a]);
+          v6[3 + a] = fmax(v6[3 + a], v[u][a]);
+        }
+  }
+#pragma unroll
+  for (int a = 0; a < 3; ++a)
+    for (int o = kWave / 2; o > 0; o >>= 1) {
+      v6[a] = fmin(v6[a], __shfl_xor(v6[a], o, kWave));
+      v6[3 + a] = fmax(v6[3 + a], __shfl_xor(v6[3 + a], o, kWave));
+    }
+  const int wid = threadIdx.x / kWave;
+  if ((threadIdx.x & (kWave - 1)) == 0)
+    for (int a = 0; a < 6; ++a) s[wid][a] = v6[a];
+  __syncthreads();
+  if (threadIdx.x < 6) {
+    const int a = threadIdx.x;
+    double r = s[0][a];
+    for (int w = 1; w < 4; ++w) r = a < 3 ? fmin(r, s[w][a]) : fmax(r, s[w][a]);
+    part[blockIdx.x * 6 + a] = r;
+  }
+}
+
+// bbox from the partials, then the grid: h for ~occ points per h^3, capped
+// at `cap` cells; the tile width of k_knn
+__global__ __launch_bounds__(256) void k_grid_params(const double *__restrict__ part,
+                                                     int nparts, size_t n, int cap,
+                                                     double occ, int sx, size_t nq,
+                                                     GridParams *gp, int *counters) {
+  // also resets the call's k-NN counters (one launch fewer than a memset)
+  if (threadIdx.x < 4) counters[threadIdx.x] = 0;
+  __shared__ double s[4][6];
+  double v6[6] = {INFINITY, INFINITY, INFINITY, -INFINITY, -INFINITY, -INFINITY};
+  for (int b = threadIdx.x; b < nparts; b += blockDim.x)
+    for (int a = 0; a < 6; ++a)
+      v6[a] = a < 3 ? fmin(v6[a], part[b * 6 + a]) : fmax(v6[a], part[b * 6 + a]);
+#pragma unroll
+  for (int a = 0; a < 3; ++a)
+    for (int o = kWave / 2; o > 0; o >>= 1) {
+      v6[a] = fmin(v6[a], __shfl_xor(v6[a], o, kWave));
+      v6[3 + a] = fmax(v6[3 + a], __shfl_xor(v6[3 + a], o, kWave));
+    }
+  if ((threadIdx.x & (kWave - 1)) == 0)
+    for (int a = 0; a < 6; ++a) s[threadIdx.x / kWave][a] = v6[a];
+  __syncthreads();
+  if (threadIdx.x != 0) return;
+  for (int w = 1; w < (int)blockDim.x / kWave; ++w)
+    for (int a = 0; a < 6; ++a)
+      v6[a] = a < 3 ? fmin(v6[a], s[w][a]) : fmax(v6[a], s[w][a]);
+  GridParams G;
+  double lo[3], ext[3];
+  bool any = n > 0;
+  for (int a = 0; a < 3; ++a) {
+    if (!(v6[a] <= v6[3 + a])) any = false;
+    lo[a] = v6[a];
+    ext[a] = v6[3 + a] - v6[a];
+  }
+  if (!any) {
+    for (int a = 0; a < 3; ++a) {
+      G.o[a] = 0.0;
+      G.g[a] = 1;
+      G.e[a] = G.inv_e[a] = 1.0;
+    }
+    G.h = G.delta = 1.0;
+    G.sx = 1;
+    G.emax = 0.0;
+    G.ncells = 1;
+    G.tile_w = 1;
+    G.clamped = 0;
+    *gp = G;
+    return;
+  }
+  const double emax = fmax(ext[0], fmax(ext[1], ext[2]));
+  const double floor_e = fmax(emax * 1e-3, 1e-9);
+  double vol = 1.0;
+  for (int a = 0; a < 3; ++a) vol *= fmax(ext[a], floor_e);
+  double h = cbrt(vol * occ / (double)n);
+  if (!(h > 0) || !(h < INFINITY)) h = fmax(emax, 1.0);
+  int g[3], clamped = 0;
+  for (int it = 0; it < 200; ++it) {
+    long long tot = 1;
+    clamped = 0;
+    for (int a = 0; a < 3; ++a) {
+      const double ea = a == 0 ? h / sx : h;
+      double ga = floor(ext[a] / ea) + 1.0;  // covers [lo, lo + ext] inclusive
+      if (ga > 2048) {
+        ga = 2048;
+        clamped = 1;
+      }
+      g[a] = (int)ga;
+      tot *= g[a];
+    }
+    if (tot <= cap) break;
+    h *= 1.1;
+  }
+  G.clamped = clamped;
+  for (int a = 0; a < 3; ++a) G.o[a] = lo[a];
+  G.h = h;
+  G.sx = sx;
+  for (int a = 0; a < 3; ++a) {
+    G.e[a] = a == 0 ? h / sx : h;
+    G.inv_e[a] = 1.0 / G.e[a];
+  }
+  G.delta = 1e-7 * (emax + h);
+  G.emax = emax;
+  G.g[0] = g[0];
+  G.g[1] = g[1];
+  G.g[2] = g[2];
+  G.ncells = g[0] * g[1] * g[2];
+  // tile width: ~kTileQueries queries per tile, and its 9 staged row
+  // segments of W + 2 sx cells within ~90 % of the LDS record budget;
+  // balanced: the fewest tiles per grid row at that width, then equal widths
+  // (a ragged last tile would pay a full staging + barrier cycle for a few
+  // cells)
+  const double occ_q = (double)nq / G.ncells, occ_t = (double)n / G.ncells;
+  double w = fmin(kTileQueries / fmax(occ_q, 1e-9),
+                  0.9 * kTileRec / (9.0 * fmax(occ_t, 1e-9)) - 2.0 * sx);
+  const int wmax = (int)fmax(1.0, fmin((double)(kTileCols - 1 - 2 * sx), floor(w)));
+  const int tpr = (G.g[0] + wmax - 1) / wmax;
+  G.tile_w = (G.g[0] + tpr - 1) / tpr;
+  *gp = G;
+}
+
+__device__ __forceinline__ int cell_axis(double v, const GridParams &G, int a) {
+  const double t = (v - G.o[a]) * G.inv_e[a];
+  if (!(t >= 0.0)) return 0;  // below the grid, or NaN
+  if (t >= (double)G.g[a]) return G.g[a] - 1;
+  return (int)t;
+}
+
+__device__ __forceinline__ int cell_of(const double *p, const GridParams &G) {
+  return (cell_axis(p[2], G, 2) * G.g[1] + cell_axis(p[1], G, 1)) * G.g[0] +
+         cell_axis(p[0], G, 0);
+}
+
+constexpr int kScanBlock = 1024, kScanPer = 4, kScanTile = kScanBlock * kScanPer;
+
+__global__ __launch_bounds__(kScanBlock) void k_scan_sums(const int *__restrict__ in, int n,
+                                                          int *__restrict__ bsum) {
+  __shared__ int scratch[40];
+  const int base = blockIdx.x * kScanTile + threadIdx.x * kScanPer;
+  int s = 0;
+#pragma unroll
+  for (int k = 0; k < kScanPer; ++k)
+    if (base + k < n) s += in[base + k];
+  int total;
+  block_excl_scan(s, scratch, &total);
+  if (threadIdx.x == 0) bsum[blockIdx.x] = total;
+}
+
+__global__ __launch_bounds__(kScanBlock) void k_scan_apply(const int *__restrict__ in, int n,
+                                                           const int *__restrict__ bsum,
+                                                           int *__restrict__ out) {
+  __shared__ int scratch[40];
+  const int base = blockIdx.x * kScanTile + threadIdx.x * kScanPer;
+  int v[kScanPer];
+  int s = 0;
+#pragma unroll
+  for (int k = 0; k < kScanPer; ++k) {
+    v[k] = base + k < n ? in[base + k] : 0;
+    s += v[k];
+  }
+  // this block's offset: the sum of the block totals before it, read straight
+  // from bsum (a separate top-level scan launch costs more than these reads)
+  int pre = 0;
+  for (int i = threadIdx.x; i < (int)blockIdx.x; i += blockDim.x) pre += bsum[i];
+  int total, ptot;
+  block_excl_scan(pre, scratch, &ptot);
+  __syncthreads();  // scratch is reused by the next scan
+  int off = block_excl_scan(s, scratch, &total) + ptot;
+#pragma unroll
+  for (int k = 0; k < kScanPer; ++k) {
+    if (base + k < n) out[base + k] = off;
+    off += v[k];
+  }
+}
+
+// ---- cell binning: counting sort of both clouds by grid cell --------------
+// Scattered global atomics run at the memory side on this part (~24 G/s
+// whatever their scope), so the sort uses none: LDS histograms and LDS ranks.
+//  k_bin_hist    each block takes a contiguous chunk of points and counts
+//                their coarse bucket (cell >> shift) in LDS; counts land in a
+//                bucket-major table[b * nblk + block], so ONE exclusive scan
+//                of the table gives every (bucket, block) its output offset.
+//  k_bin_scatter same chunks: each point gets an LDS rank within its
+//                (bucket, block) and moves to the coarse-bucketed array.
+//  k_bin_fine    one block per bucket: LDS counting sort over the bucket's
+//                2^shift cells, writes start[] for them and every point at its
+//                final cell-sorted position as a PRec. Order inside a cell is
+//                unspecified: the k-NN result does not depend on it (ties are
+//                resolved by (distance, index) in the exact stage).
+// Side 0 = targets, side 1 = queries; both go through the same launches
+// (block ranges) and their tables are concatenated so one scan covers both.
+struct BinPt {
+  double x, y, z;
+  int idx, cell;
+};
+struct BinSide {
+  const double *p;
+  int n, P, nblk;
+  int tab;  // offset of this side's table in the concatenated table
+  int sub;  // subtracted from scanned offsets (targets' total, for side 1)
+  int *start;
+  BinPt *bin;   // coarse-bucketed
+  PRec *sorted; // cell-sorted
+};
+struct BinJob {
+  BinSide s[2];
+  int shift, nb;  // buckets per side
+};
+constexpr int kBinMaxBuckets = 4096;
+constexpr int kBinMaxShift = 15;
+constexpr int kBinUnroll = 8;  // points per thread with loads in flight
+constexpr int kBinP = 4096;    // minimum points per k_bin_hist / k_bin_scatter block
+constexpr int kBinMinShift = 10;  // coarse buckets of 2^10 cells (r2 A/B)
+constexpr int kBinFineThreads = 512;
+constexpr int kBinFineHold = 4096 / kBinFineThreads;  // points per thread held in registers
+
+__device__ __forceinline__ int bin_side(const BinJob &J, int &blk) {
+  const int side = blk >= J.s[0].nblk ? 1 : 0;
+  if (side) blk -= J.s[0].nblk;
+  return side;
+}
+
+struct P3 {
+  double x, y, z;
+};
+
+// the block's chunk in batches of kBinUnroll points per thread: every load of
+// a batch is issued before any of its cells is used
+template <class F>
+__device__ __forceinline__ void bin_chunk(const BinSide &S, int blk, const GridParams &G, F f) {
+  const int i0 = blk * S.P, i1 = min(S.n, (blk + 1) * S.P);
+  const int bd = (int)blockDim.x;
+  for (int ib = i0; ib < i1; ib += kBinUnroll * bd) {
+    P3 v[kBinUnroll];
+#pragma unroll
+    for (int u = 0; u < kBinUnroll; ++u) {
+      const int i = ib + u * bd + (int)threadIdx.x;
+      if (i < i1) v[u] = *(const P3 *)(S.p + 3 * (size_t)i);
+    }
+#pragma unroll
+    for (int u = 0; u < kBinUnroll; ++u) {
+      const int i = ib + u * bd + (int)threadIdx.x;
+      if (i < i1) f(i, v[u], cell_of(&v[u].x, G));
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void k_bin_hist(BinJob J, const GridParams *__restrict__ gp,
+                                                  int *__restrict__ table) {
+  __shared__ int hist[kBinMaxBuckets];
+  int blk = blockIdx.x;
+  const BinSide S = J.s[bin_side(J, blk)];
+  const GridParams G = *gp;
+  for (int b = threadIdx.x; b < J.nb; b += blockDim.x) hist[b] = 0;
+  __syncthreads();
+  bin_chunk(S, blk, G, [&](int, const P3 &, int c) { atomicAdd(&hist[c >> J.shift], 1); });
+  __syncthreads();
+  for (int b = threadIdx.x; b < J.nb; b += blockDim.x) table[S.tab + b * S.nblk + blk] = hist[b];
+  if (blk == 0 && threadIdx.x == 0) table[S.tab + J.nb * S.nblk] = 0;  // sentinel
+}
+
+__global__ __launch_bounds__(256) void k_bin_scatter(BinJob J, const GridParams *__restrict__ gp,
+                                                     const int *__restrict__ offs) {
+  __shared__ int cur[kBinMaxBuckets];
+  int blk = blockIdx.x;
+  const BinSide S = J.s[bin_side(J, blk)];
+  const GridParams G = *gp;
+  for (int b = threadIdx.x; b < J.nb; b += blockDim.x)
+    cur[b] = offs[S.tab + b * S.nblk + blk] - S.sub;
+  __syncthreads();
+  bin_chunk(S, blk, G, [&](int i, const P3 &v, int c) {
+    const int pos = atomicAdd(&cur[c >> J.shift], 1);
+    BinPt t;
+    t.x = v.x;
+    t.y = v.y;
+    t.z = v.z;
+    t.idx = i;
+    t.cell = c;
+    S.bin[pos] = t;
+  });
+}
+
+// One bucket: count its points per cell (LDS), scan, write the cell starts,
+// then place every point. The first kBinFineHold * blockDim points stay in
+// registers between the count and the placement (one global read, not two);
+// a larger bucket re-reads the rest.
+__global__ __launch_bounds__(kBinFineThreads) void k_bin_fine(BinJob J,
+                                                              const GridParams *__restrict__ gp,
+                                                              const int *__restrict__ offs,
+                                                              int nscan) {
+  extern __shared__ int cnt[];  // 2^shift
+  __shared__ int scratch[40];
+  const int side = blockIdx.x >= J.nb ? 1 : 0;
+  const int b = blockIdx.x - (side ? J.nb : 0);
+  const BinSide S = J.s[side];
+  const int ncell = 1 << J.shift, base = b << J.shift;
+  const int lo = offs[S.tab + b * S.nblk] - S.sub;
+  const int hi = offs[S.tab + (b + 1) * S.nblk] - S.sub;
+  const BinPt *src = S.bin;
+  for (int j = threadIdx.x; j < ncell; j += blockDim.x) cnt[j] = 0;
+  __syncthreads();
+  BinPt hold[kBinFineHold];
+  const int bd = (int)blockDim.x, held_end = min(hi, lo + kBinFineHold * bd);
+#pragma unroll
+  for (int u = 0; u < kBinFineHold; ++u) {
+    const int i = lo + u * bd + (int)threadIdx.x;
+    if (i < held_end) hold[u] = src[i];
+  }
+#pragma unroll
+  for (int u = 0; u < kBinFineHold; ++u) {
+    const int i = lo + u * bd + (int)threadIdx.x;
+    if (i < held_end) atomicAdd(&cnt[hold[u].cell - base], 1);
+  }
+  for (int i = held_end + (int)threadIdx.x; i < hi; i += bd) atomicAdd(&cnt[src[i].cell - base], 1);
+  __syncthreads();
+  // exclusive scan over the bucket's cells: each thread owns a contiguous run
+  const int per = ncell / bd;  // ncell is a multiple of the block size
+  const int j0 = (int)threadIdx.x * per;
+  int sum = 0;
+  for (int u = 0; u < per; ++u) sum += cnt[j0 + u];
+  int total;
+  int acc = lo + block_excl_scan(sum, scratch, &total);
+  for (int u = 0; u < per; ++u) {
+    const int v = cnt[j0 + u];
+    cnt[j0 + u] = acc;
+    if (base + j0 + u < nscan) S.start[base + j0 + u] = acc;
+    acc += v;
+  }
+  __syncthreads();
+  const int g0 = gp->g[0];
+  auto place = [&](const BinPt &e) {
+    const int pos = atomicAdd(&cnt[e.cell - base], 1);
+    PRec t;
+    t.x = e.x;
+    t.y = e.y;
+    t.z = e.z;
+    t.idx = e.idx;
+    t.cx = e.cell % g0;
+    S.sorted[pos] = t;
+  };
+#pragma unroll
+  for (int u = 0; u < kBinFineHold; ++u) {
+    const int i = lo + u * bd + (int)threadIdx.x;
+    if (i < held_end) place(hold[u]);
+  }
+  for (int i = held_end + (int)threadIdx.x; i < hi; i += bd) place(src[i]);
+}
+
+// ============================================================ k-NN helpers
+// (d, i) < (kd, ki): distance first, then index. Never true for d = inf/NaN.
+__device__ __forceinline__ bool knn_less(double d, int i, double kd, int ki) {
+  return d < kd || (d == kd && i < ki);
+}
+
+// the same without short-circuit evaluation (selects, no branches)
+__device__ __forceinline__ bool knn_less_bf(double d, int i, double kd, int ki) {
+  return (d < kd) | ((d == kd) & (i < ki));
+}
+
+// compare-exchange: (ad, ai) <= (bd, bi) by (distance, index) afterwards
+__device__ __forceinline__ void knn_cx(double &ad, int &ai, double &bd, int &bi) {
+  const bool sw = knn_less_bf(bd, bi, ad, ai);
+  const double td = sw ? bd : ad, ud = sw ? ad : bd;
+  const int ti = sw ? bi : ai, ui = sw ? ai : bi;
+  ad = td;
+  ai = ti;
+  bd = ud;
+  bi = ui;
+}
+
+// squared distance from q to the box of cells [x0..x1] x [y0..y1] x [z0..z1]
+// grown by delta: a lower bound on the reference dsq of any point binned there
+__device__ __forceinline__ double box_d2(const GridParams &G, const double *qv, int x0, int x1,
+                                         int y0, int y1, int z0, int z1) {
+  const int lo[3] = {x0, y0, z0}, hi[3] = {x1, y1, z1};
+  double s = 0.0;
+#pragma unroll
+  for (int a = 0; a < 3; ++a) {
+    const double bl = G.o[a] + lo[a] * G.e[a] - G.delta;
+    const double bh = G.o[a] + (hi[a] + 1) * G.e[a] + G.delta;
+    // boundary cells also hold everything clamped into them
+    const double e = fmax(0.0, fmax(lo[a] > 0 ? bl - qv[a] : 0.0,
+                                     hi[a] < G.g[a] - 1 ? qv[a] - bh : 0.0));
+    s += e * e;
+  }
+  return s;
+}
+
+// Distance from q (in cell c) to the outside of its block of radius r: cells
+// x - r sx .. x + r sx, y - r .. y + r, z - r .. z + r. A block face on the
+// grid boundary does not count (the boundary cells hold everything clamped
+// into them); INFINITY when every face is.
+__device__ __forceinline__ double block_reach(const GridParams &G, const double *qv,
+                                              const int c[3], int r) {
+  double L = INFINITY;
+#pragma unroll
+  for (int a = 0; a < 3; ++a) {
+    const int ra = a == 0 ? r * G.sx : r;
+    if (c[a] - ra > 0) L = fmin(L, qv[a] - (G.o[a] + (c[a] - ra) * G.e[a]));
+    if (c[a] + ra < G.g[a] - 1) L = fmin(L, (G.o[a] + (c[a] + ra + 1) * G.e[a]) - qv[a]);
+  }
+  return L;
+}
+
+// Error of the packed-f32 squared distance: each coordinate is rounded to f32
+// once relative to the tile origin (<= 2^-24 |v|) and subtracted once in f32,
+// so each difference is within dl = Dq 2^-22 of the exact one (Dq bounds the
+// magnitudes); then |d2_f32 - d2| <= err(d2_f32-ish) below.
+__device__ __forceinline__ double f32_err(double V, double dl) {
+  return V * 0x1p-20 + 4.0 * dl * __builtin_sqrt(V) + 4.0 * dl * dl;
+}
+
+// f32 admission bound for an f64 dsq bound T: every candidate whose exact
+// dsq is <= T has an f32 dsq <= the returned value.
+__device__ __forceinline__ float f32_bound(double T, double dl) {
+  if (!(T < INFINITY)) return INFINITY;
+  const double E = T * 0x1p-20 + 4.0 * dl * __builtin_sqrt(T) + 4.0 * dl * dl;
+  return (float)((T + E) * (1.0 + 0x1p-20));
+}
+
+__device__ __forceinline__ uint32_t umed3(uint32_t a, uint32_t b, uint32_t c) {
+  return max(min(a, b), min(max(a, b), c));  // one v_med3_u32
+}
+
+// key = (f32 distance bits with the low kKeyBits cleared) | local id, as ONE
+// v_and_or_b32 (the mask in a VGPR, the id in an SGPR). lid MUST be
+// wave-uniform: a divergent value would be read from the first lane only.
+__device__ __forceinline__ uint32_t knn_key(float d, uint32_t vmask, uint32_t lid) {
+  uint32_t k;
+  asm("v_and_or_b32 %0, %1, %2, %3" : "=v"(k) : "v"(__float_as_uint(d)), "v"(vmask), "s"(lid));
+  return k;
+}
+
+typedef float f2 __attribute__((ext_vector_type(2)));
+
+struct KnnLists {
+  int *slow_q, *n_slow;  // queries (cell-sorted positions) the fast path could not certify
+  double *slow_thr;      // their starting bound (K-th dsq upper bound), or inf
+  int *n_unstaged;       // of them: queries whose block exceeded the LDS budget
+  int vec_out;           // outputs 16-B aligned: results may be stored as vectors
+};
+
+__device__ __forceinline__ void push_slow(const KnnLists &L_, int qi, double thr) {
+  const int e = atomicAdd(L_.n_slow, 1);
+  L_.slow_q[e] = qi;
+  L_.slow_thr[e] = thr;
+}
+
+// ============================================================ k_knn
+// Global-mode exact k-NN over tiles of W consecutive x cells of one grid row.
+// Cells are h/sx wide in x and h in y, z, so a query's block (cells x-sx ..
+// x+sx, y-1 .. y+1, z-1 .. z+1) reaches >= h from it on every axis while
+// spanning only (2 sx + 1)/sx h in x.
+//
+// Staging. A tile stages the 9 neighbouring row segments (cells xa-sx ..
+// xb+sx) into LDS COLUMN-major: for each x cell j, the records of its 9
+// (y, z) rows follow one another, so a query's block is ONE contiguous slot
+// range [colst[i], colst[i + 2 sx + 1]). Each record is the f32 offset of the
+// f64 point from the tile's centre (x, y, z) and its cell-sorted position g,
+// in two pair-interleaved planes of 16 B per pair of records: XY (x0 x1 y0 y1)
+// and ZG (z0 z1 g0 g1). A tile whose segments exceed the LDS budget is cut
+// into narrower sub-ranges of query cells; a single cell whose block alone
+// exceeds it sends its queries to k_knn_slow.
+//
+// One query per lane (cell-sorted queries, read coalesced). The block is
+// walked in pairs of records from its even-aligned first slot ta: packed f32
+// squared distances (3 packed sub, 1 mul, 2 fma per pair), keys packed with
+// the wave-uniform pair offset as local id. A key enters the lane's LDS list
+// only if it is below the lane's threshold T: at first the f32 image of R^2,
+// R the radius holding ~lambda targets at the block's density; after each
+// drain, the (K+1)-th key of the lane's sorted list. A drain (when some lane's
+// list is nearly full, and at the end) inserts the listed keys into the sorted
+// K+1 smallest by a branch-free median-of-3 network. So the network runs on
+// the ~lambda survivors, not on all ~100 candidates of the block.
+//
+// Exact stage and certificate. The K best keys are re-evaluated with the
+// reference f64 formula from the cell-sorted f64 copy and ordered by
+// (distance, index). Every candidate left out is bounded below: outside the
+// block by the block's reach, rejected against the first threshold by R^2,
+// rejected or evicted later by the (K+1)-th key V minus the f32 error. If
+// that bound exceeds the K-th exact dsq (times 1 + 2^-46), the answer is
+// exact; otherwise the query goes to k_knn_slow with the K-th dsq as bound.
+template <int K>
+__global__ __launch_bounds__(kTileThreads, 4) void k_knn(
+    const GridParams *__restrict__ gp, const int *__restrict__ tstart,
+    const PRec *__restrict__ tsort, const int *__restrict__ qstart,
+    const PRec *__restrict__ qsort, int32_t *__restrict__ oidx, double *__restrict__ odist,
+    KnnLists L_, float lambda) {
+  __shared__ __attribute__((aligned(16))) float spair[2 * kZgOff];
+  // cbr[r][j]: the LDS slot of the record at cell-sorted position g of cell
+  // (row r, tile column j) is cbr[r][j] + g - sbase. Before that: the row
+  // segments' global starts (soff)
+  __shared__ int cbr[9][kTileCols];
+  __shared__ int colst[kTileCols];  // first slot of tile column j (whole tile)
+  __shared__ uint32_t slist[kList ? kListCap * kTileThreads : 1];
+  __shared__ int seg[9][2];  // each row segment's global [first, end)
+  __shared__ int scratch[kTileThreads / kWave + 1];
+  constexpr int KL = K + 1;
+  static_assert(K >= 1 && K <= 16, "K");
+  const GridParams G = *gp;
+  const int W = G.tile_w, S = G.sx;
+  const int tpr = (G.g[0] + W - 1) / W;
+  const int ntiles = tpr * G.g[1] * G.g[2];  // < cells < 2^31
+  // tiles dealt to the 8 XCDs in contiguous ranges (block b runs on XCD
+  // b % 8 under the observed round-robin placement; another placement only
+  // costs L2 hits), so each XCD's L2 holds only its slab of the cloud
+  const int xcd = blockIdx.x & 7;
+  const int t_hi = (int)((long long)ntiles * (xcd + 1) / 8);
+  const int tid = (int)threadIdx.x;
+  const int lane = tid & (kWave - 1), wv = tid / kWave;
+  const uint32_t vmask = ~kKeyMask;
+  NV_ACC_DECL;
+  // volume of a query's block, in units of h^3
+  const float vol_h3 = 9.0f * (float)(2 * S + 1) / (float)S;
+  for (int tile = (int)((long long)ntiles * xcd / 8) + (int)(blockIdx.x >> 3); tile < t_hi;
+       tile += (int)(gridDim.x >> 3)) {
+    NV_STAMP(tb0);
+    const int row = tile / tpr, chunk = tile - row * tpr;
+    const int y = row % G.g[1], z = row / G.g[1];
+    const int xa = chunk * W, xb = min(xa + W, G.g[0]) - 1;
+    const int ncol = xb - xa + 1 + 2 * S;  // tile columns j: cells xa - S + j
+    // tile centre: the f32 records are offsets from it
+    const double ot[3] = {G.o[0] + (xa + 0.5 * (xb - xa + 1)) * G.e[0],
+                          G.o[1] + (y + 0.5) * G.h, G.o[2] + (z + 0.5) * G.h};
+    // largest staged offset magnitude (cell-assignment slack included)
+    // (a clamped grid's boundary cells may hold anything inside the bbox)
+    const double Dt = G.clamped ? G.emax + 2.0 * G.h
+                                : fmax((0.5 * (xb - xa + 1) + S + 1) * G.e[0], 2.0 * G.h) +
+                                      4.0 * G.delta;
+    // ---- the 9 row segments' starts: soff[r][j] for j = 0 .. ncol (the
+    // row's end for cells past the grid)
+    if (tid <= ncol) {
+      int v[9];
+#pragma unroll
+      for (int r = 0; r < 9; ++r) {
+        const int yy = y + (r % 3) - 1, zz = z + (r / 3) - 1;
+        v[r] = 0;
+        if (yy >= 0 && yy < G.g[1] && zz >= 0 && zz < G.g[2]) {
+          const int x = min(max(xa - S + tid, 0), G.g[0]);  // x = g0: the row's end
+          v[r] = tstart[(zz * G.g[1] + yy) * G.g[0] + x];
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < 9; ++r) cbr[r][tid] = v[r];
+    }
+    __syncthreads();
+    // ---- column counts, their exclusive scan (colst), and cbr in place
+    {
+      const int j = tid;
+      int sv[9], n[9], cs = 0;
+#pragma unroll
+      for (int r = 0; r < 9; ++r) {
+        sv[r] = j < ncol ? cbr[r][j] : 0;
+        n[r] = j < ncol ? cbr[r][j + 1] - sv[r] : 0;
+        cs += n[r];
+      }
+      if (j < 9) {
+        seg[j][0] = cbr[j][0];
+        seg[j][1] = cbr[j][ncol];
+      }
+      int total;
+      const int cex = block_excl_scan(cs, scratch, &total);  // barriers: cbr reads done
+      if (j <= ncol) colst[j] = cex;  // colst[ncol] = the total
+      if (j < ncol) {
+        int a = cex;
+#pragma unroll
+        for (int r = 0; r < 9; ++r) {
+          cbr[r][j] = a - sv[r];
+          a += n[r];
+        }
+      }
+    }
+    __syncthreads();
+    const int cell0 = (z * G.g[1] + y) * G.g[0] + xa - S;  // cell of tile column 0
+    // ---- sub-ranges of query columns [qa, qb] (tile columns S .. ncol-1-S)
+    // whose staged columns [qa - S, qb + S] fit the LDS budget; one
+    // sub-range unless the tile is unusually dense
+    for (int qa = S; qa <= ncol - 1 - S;) {
+      const int base0 = colst[qa - S];
+      const bool fits = tid >= qa && tid <= ncol - 1 - S && colst[tid + S + 1] - base0 <= kTileRec;
+      const int qb = qa - 1 + __syncthreads_count(fits);  // fits is a prefix of [qa, ..]
+      if (qb < qa) {
+        // one query cell whose block alone exceeds the budget: its queries
+        // go to k_knn_slow from an infinite bound
+        const int q0 = qstart[cell0 + qa], q1 = qstart[cell0 + qa + 1];
+        for (int qi = q0 + tid; qi < q1; qi += kTileThreads) {
+          push_slow(L_, qi, INFINITY);
+          atomicAdd(L_.n_unstaged, 1);
+        }
+        ++qa;
+        continue;
+      }
+      const int ja = qa - S, jb = qb + S;
+      const int sbase = colst[ja];
+      // ---- copy: each wave takes whole row segments (r = wave, wave + 3,
+      // wave + 6), so a record's row is wave-uniform; all loads of a batch
+      // are issued before any LDS write. Records outside [ja, jb] (a cut
+      // tile) are skipped.
+      constexpr int U = 2;
+      for (int r = wv; r < 9; r += kTileThreads / kWave) {
+        const int g0 = seg[r][0], nr = seg[r][1] - g0;
+        const int *cb = &cbr[r][0];
+        for (int k0 = 0; k0 < nr; k0 += U * kWave) {
+          PRec v[U];
+#pragma unroll
+          for (int u = 0; u < U; ++u) {
+            const int k = k0 + u * kWave + lane;
+            if (k < nr) v[u] = tsort[g0 + k];
+          }
+#pragma unroll
+          for (int u = 0; u < U; ++u) {
+            const int k = k0 + u * kWave + lane;
+            // the record's tile column (its cell lies in xa-S .. xb+S)
+            const int jj = v[u].cx - (xa - S);
+            if (k < nr && jj >= ja && jj <= jb) {
+              const int g = g0 + k;
+              const int slot = cb[jj] + g - sbase;
+              float *d = spair + (slot >> 1) * 4 + (slot & 1);
+              d[0] = (float)(v[u].x - ot[0]);
+              d[2] = (float)(v[u].y - ot[1]);
+              d[kZgOff] = (float)(v[u].z - ot[2]);
+              d[kZgOff + 2] = __int_as_float(g);
+            }
+          }
+        }
+      }
+      __syncthreads();
+      NV_STAMP(tb1);
+      NV_ACC(1, tb0, tb1);
+      // ---- the sub-range's queries
+      const int q0 = qstart[cell0 + qa], q1 = qstart[cell0 + qb + 1];
+      for (int qi = q0 + tid; qi < q1 && !(kAbl & kAblNoQuery); qi += kTileThreads) {
+        NV_STAMP(ts0);
+        const PRec Q = qsort[qi];
+        const double qv[3] = {Q.x, Q.y, Q.z};
+        const int c[3] = {Q.cx, y, z};
+        const int i = Q.cx - (xa - S);  // tile column of the query's cell
+        const int t0 = colst[i - S] - sbase, t1 = colst[i + S + 1] - sbase;
+        const double qr[3] = {qv[0] - ot[0], qv[1] - ot[1], qv[2] - ot[2]};
+        const double Dq = fmax(Dt, fmax(fabs(qr[0]), fmax(fabs(qr[1]), fabs(qr[2]))));
+        const double dl = Dq * 0x1p-22;
+        const f2 qx2 = {(float)qr[0], (float)qr[0]}, qy2 = {(float)qr[1], (float)qr[1]},
+                 qz2 = {(float)qr[2], (float)qr[2]};
+        // first threshold: R^2 with R holding ~lambda targets at the block's
+        // density (R^3 = 3 lambda vol / (4 pi count))
+        // (none when the block reaches every face of the grid: then it holds
+        // every target and nothing needs filtering)
+        const int count = t1 - t0;
+        const double Lr = block_reach(G, qv, c, 1);
+        double Tgeo = INFINITY;
+        if (kList && count > 0 && Lr < INFINITY) {
+          const float r3 = 0.2387324146f * lambda * vol_h3 / (float)count;  // 3/(4 pi)
+          Tgeo = (double)__builtin_amdgcn_exp2f(__builtin_amdgcn_logf(r3) * (2.0f / 3.0f)) *
+                 (G.h * G.h);
+        }
+        const float Tf = f32_bound(Tgeo, dl);
+        uint32_t T = Tf < INFINITY ? (__float_as_uint(Tf) | kKeyMask) + 1u : kNoKey;
+        uint32_t key[KL];
+#pragma unroll
+        for (int s = 0; s < KL; ++s) key[s] = kNoKey;
+        auto ins = [&](uint32_t kk) {  // keep the K+1 smallest keys sorted
+#pragma unroll
+          for (int s = K; s > 0; --s) key[s] = umed3(key[s - 1], key[s], kk);
+          key[0] = min(key[0], kk);
+        };
+        // the lane's survivor list: entry e at slist[e * kTileThreads + tid];
+        // lo = the next free entry's offset
+        uint32_t *const lst = slist + tid;
+        int lo = 0;
+        auto drain = [&]() {
+          if constexpr (!kList) return;
+          const int cnt = lo / kTileThreads;
+          NV_STAMP(td0);
+          if (__any(cnt > 0)) {
+            int e = 0;
+            do {
+              NV_ACC(9, 0ull, 1ull);
+              const uint32_t v = lst[e * kTileThreads];  // stale past cnt: masked below
+              ins(e < cnt ? v : kNoKey);
+              ++e;
+            } while (__any(e < cnt));
+          }
+          lo = 0;
+          T = min(T, key[K]);
+          NV_STAMP(td1);
+          NV_ACC(10, td0, td1);
+        };
+        // branch-free append: the key is always written at the free entry
+        // and the entry kept only if it passes (no exec-mask juggling in the
+        // scan loop); a drain keeps lo <= (kListCap - 2) entries before a pair
+        auto offer = [&](uint32_t kk) {
+          if constexpr (kList) {
+            lst[lo] = kk;
+            lo += kk < T ? kTileThreads : 0;
+          } else {
+            ins(kk);
+          }
+        };
+        auto nearly_full = [&]() { return kList && lo > (kListCap - 2) * kTileThreads; };
+        auto dist2 = [&](const float *p) {  // packed f32 squared distances of a pair
+          const float4 xy = *(const float4 *)p;
+          const float2 zz = *(const float2 *)(p + kZgOff);
+          const f2 fx2 = f2{xy.x, xy.y} - qx2, fy2 = f2{xy.z, xy.w} - qy2,
+                   fz2 = f2{zz.x, zz.y} - qz2;
+          return __builtin_elementwise_fma(fz2, fz2,
+                                           __builtin_elementwise_fma(fy2, fy2, fx2 * fx2));
+        };
+        NV_STAMP(ts1);
+        const int ta = t0 & ~1;
+        const int np = (t1 - ta + 1) >> 1;  // pairs the block touches
+        const bool overflow = (t1 - ta) > (1 << kKeyBits);
+        const float *cur = spair + (ta >> 1) * 4;
+        if (np > 0) {  // first pair: may start before the block (odd t0) or end past it
+          const f2 d = dist2(cur);
+          const uint32_t k0 = knn_key(d[0], vmask, 0u), k1 = knn_key(d[1], vmask, 1u);
+          if (ta >= t0) offer(k0);
+          if (ta + 1 < t1) offer(k1);
+          cur += 4;
+        }
+        // interior pairs: both records inside the block; the key's local id
+        // is the wave-uniform pair counter. A lane leaves at its last pair.
+        if (np > 2) {
+          const float *last = spair + ((ta >> 1) + np - 1) * 4;
+          uint32_t v2 = 2;
+          do {
+            const f2 d = dist2(cur);
+            offer(knn_key(d[0], vmask, v2));
+            offer(knn_key(d[1], vmask, v2 + 1));
+            cur += 4;
+            v2 += 2;
+            if (__any(nearly_full())) drain();
+          } while (cur < last);
+        }
+        if (np > 1) {  // last pair: may end past the block
+          const f2 d = dist2(cur);
+          const uint32_t lid = (uint32_t)(2 * (np - 1)) & kKeyMask;
+          // lid depends on the lane's np here: the plain and + or
+          const uint32_t k0 = (__float_as_uint(d[0]) & vmask) | lid;
+          const uint32_t k1 = (__float_as_uint(d[1]) & vmask) | (lid + 1);
+          if (__any(nearly_full())) drain();
+          offer(k0);
+          if (ta + 2 * (np - 1) + 1 < t1) offer(k1);
+        }
+        drain();
+        NV_STAMP(ts2);
+        // ---- certificate bound on every candidate left out
+        double B = INFINITY;
+        if (Lr < INFINITY) {
+          const double Lg = Lr - 2.0 * G.delta;
+          B = Lg > 0.0 ? Lg * Lg : 0.0;
+        }
+        B = fmin(B, Tgeo);  // rejected against the first threshold: exact dsq > Tgeo
+        if (key[K] != kNoKey) {
+          const double V = (double)__uint_as_float(key[K] & vmask);
+          B = fmin(B, V - f32_err(V, dl));
+        }
+        bool ok = !overflow && Dq < 1e17;
+        if (kAbl & kAblNoExact) {  // timing-only: keep the keys live, one store
+          uint32_t acc = 0;
+#pragma unroll
+          for (int s = 0; s < KL; ++s) acc ^= key[s];
+          oidx[(size_t)Q.idx * K] = (int)acc + (int)B;
+          continue;
+        }
+        // ---- exact f64 stage on the K best keys. All loads are issued
+        // unconditionally (an empty slot re-reads slot 0) so their latencies
+        // overlap; coordinates from the cell-sorted copy (L2-local).
+        double ed[K];
+        int ei[K];
+        {
+          int gpos[K];
+#pragma unroll
+          for (int s = 0; s < K; ++s) {
+            const uint32_t kk = key[s] != kNoKey ? key[s] : key[0];
+            // clamped into the block so a corrupt id can never leave the tile
+            const int p = min(max(ta + (int)(kk & kKeyMask), t0), max(t1 - 1, t0));
+            gpos[s] = __float_as_int(spair[kZgOff + (p >> 1) * 4 + 2 + (p & 1)]);
+          }
+#pragma unroll
+          for (int s = 0; s < K; ++s) {
+            const bool val = key[s] != kNoKey && count > 0;
+            // x, y as one 16-B load, z and idx as an 8-B and a 4-B load
+            const PRec *tp = tsort + gpos[s];
+            const double2 xy = *(const double2 *)&tp->x;
+            const double pz = tp->z;
+            const int pid = tp->idx;
+            const double ddx = xy.x - qv[0], ddy = xy.y - qv[1], ddz = pz - qv[2];
+            const double dsq = ddx * ddx + ddy * ddy + ddz * ddz;  // utils/kdtree.c:16
+            ei[s] = val ? pid : -1;
+            ed[s] = val ? __builtin_sqrt(dsq) : INFINITY;
+            // an inf/NaN distance is never a neighbour (kdtree.c:117)
+            if (val && !(ed[s] < INFINITY)) {
+              ed[s] = INFINITY;
+              ei[s] = -1;
+              ok = false;
+            }
+          }
+        }
+        // order by (distance, index): the truncated-key order is almost always
+        // right and a misordered survivor sits next to its place; bubble
+        // passes (branch-free compare-exchange) run until no lane of the wave
+        // is out of order, usually none
+        bool sorted = true;
+#pragma unroll
+        for (int s = 1; s < K; ++s) sorted &= !knn_less_bf(ed[s], ei[s], ed[s - 1], ei[s - 1]);
+        for (int pass = 0; pass < K - 1 && __any(!sorted); ++pass) {
+#pragma unroll
+          for (int u = 1; u < K; ++u) knn_cx(ed[u - 1], ei[u - 1], ed[u], ei[u]);
+          sorted = true;
+#pragma unroll
+          for (int s = 1; s < K; ++s) sorted &= !knn_less_bf(ed[s], ei[s], ed[s - 1], ei[s - 1]);
+        }
+        const double dk = ed[K - 1];
+        const double dk2 = dk * dk;  // >= the exact K-th dsq (sqrt rounds to nearest)
+        if (dk < INFINITY)
+          ok = ok && B > dk2 * (1.0 + 0x1p-46);
+        else
+          ok = ok && B == INFINITY;  // fewer than K neighbours: only if all was seen
+        if (ok) {
+          const size_t q = (size_t)Q.idx;
+          // a query's K results are contiguous: 16-B stores when K allows and
+          // the host found both outputs 16-B aligned (L_.vec_out)
+          if (K % 4 == 0 && L_.vec_out) {
+#pragma unroll
+            for (int s = 0; s < K; s += 4)
+              *(int4 *)(oidx + q * K + s) = make_int4(ei[s], ei[s + 1], ei[s + 2], ei[s + 3]);
+#pragma unroll
+            for (int s = 0; s < K; s += 2)
+              *(double2 *)(odist + q * K + s) = make_double2(ed[s], ed[s + 1]);
+          } else {
+#pragma unroll
+            for (int s = 0; s < K; ++s) {
+              oidx[q * K + s] = ei[s];
+              odist[q * K + s] = ed[s];
+            }
+          }
+        } else {
+          // K listed points have dsq <= dk2: a valid starting bound for the
+          // slow path. Not after an overfull block: its keys' offsets
+          // wrapped, so two slots can decode to the same record and the list
+          // may hold fewer than K distinct points.
+          push_slow(L_, qi, (dk < INFINITY && !overflow) ? dk2 * (1.0 + 0x1p-46) : INFINITY);
+        }
+        NV_STAMP(ts3);
+        NV_ACC(8, ts0, ts1);
+        NV_ACC(3, ts1, ts2);
+        NV_ACC(4, ts2, ts3);
+        NV_ACC(5, 0ull, 1ull);
+      }
+      NV_STAMP(tb2);
+      __syncthreads();  // LDS is restaged by the next sub-range or tile
+      NV_STAMP(tb3);
+      NV_ACC(2, tb1, tb2);
+      NV_ACC(7, tb2, tb3);
+      NV_ACC(6, 0ull, 1ull);
+      qa = qb + 1;
+    }
+  }
+  NV_ACC_FLUSH;
+}
+
+// ============================================================ k_knn_slow
+// insert (d, id) into the sorted exact list kd/ki if it ranks among the K
+template <int K>
+__device__ __forceinline__ void knn_insert(double *kd, int *ki, double d, int id) {
+  if (!knn_less(d, id, kd[K - 1], ki[K - 1])) return;
+  bool placed = false;
+#pragma unroll
+  for (int s = K - 1; s >= 0; --s) {
+    if (!placed) {
+      if (s > 0 && knn_less(d, id, kd[s - 1], ki[s - 1])) {
+        kd[s] = kd[s - 1];
+        ki[s] = ki[s - 1];
+      } else {
+        kd[s] = d;
+        ki[s] = id;
+        placed = true;
+      }
+    }
+  }
+}
+
+// merge the 64 lane lists kd/ki (each sorted) into md/mi: K rounds of a
+// wave (distance, index) argmin on the list heads
+template <int K>
+__device__ __forceinline__ void knn_wave_merge(double *kd, int *ki, double *md, int *mi,
+                                               int lane) {
+#pragma unroll
+  for (int s = 0; s < K; ++s) {
+    double bd = kd[0];
+    int bi = ki[0], bl = lane;
+#pragma unroll
+    for (int o = kWave / 2; o > 0; o >>= 1) {
+      const double od = __shfl_xor(bd, o, kWave);
+      const int oi = __shfl_xor(bi, o, kWave), ol = __shfl_xor(bl, o, kWave);
+      const bool take = knn_less(od, oi, bd, bi) || (!knn_less(bd, bi, od, oi) && ol < bl);
+      bd = take ? od : bd;
+      bi = take ? oi : bi;
+      bl = take ? ol : bl;
+    }
+    md[s] = bd;
+    mi[s] = bi;
+    if (lane == bl) {  // pop the winner's head
+#pragma unroll
+      for (int u = 0; u < K - 1; ++u) {
+        kd[u] = kd[u + 1];
+        ki[u] = ki[u + 1];
+      }
+      kd[K - 1] = INFINITY;
+      ki[K - 1] = -1;
+    }
+  }
+}
+
+// the reference f64 distance of record t; inserted into the lane's sorted
+// list when its dsq is within thr
+template <int K>
+__device__ __forceinline__ void knn_visit(const PRec &tp, const double qv[3], double thr,
+                                          double *kd, int *ki) {
+  const double ddx = tp.x - qv[0], ddy = tp.y - qv[1], ddz = tp.z - qv[2];
+  const double dsq = ddx * ddx + ddy * ddy + ddz * ddz;  // utils/kdtree.c:16
+  if (!(dsq <= thr)) return;
+  knn_insert<K>(kd, ki, __builtin_sqrt(dsq), tp.idx);
+}
+
+constexpr int kSlowMaxR = 3;  // one-shot cube: at most (2R+1)^2 = 49 rows
+
+// The queries k_knn could not certify, one WAVE per query, from the recorded
+// starting bound thr (K real points lie within it, so every neighbour does).
+// One-shot cube: the smallest cube of cells around the query whose outside is
+// provably beyond thr; its (y, z) rows are contiguous record ranges, counted
+// and prefix-summed across the wave so the records are dealt evenly over the
+// 64 lanes. Each lane keeps a sorted list (reference f64 distance); one wave
+// merge gives the answer. An infinite bound, or a cube beyond kSlowMaxR,
+// takes the ring search: rings of cells split over the lanes, merged after
+// every ring, the merged K-th bounding the next ring.
+template <int K>
+__global__ __launch_bounds__(256) void k_knn_slow(const GridParams *__restrict__ gp,
+                                                  const int *__restrict__ start,
+                                                  const PRec *__restrict__ tsort,
+                                                  const PRec *__restrict__ qsort,
+                                                  int32_t *__restrict__ oidx,
+                                                  double *__restrict__ odist, KnnLists L_) {
+  __shared__ double sd[4][kWave];  // per-wave survivor buffers (256 threads)
+  __shared__ int si[4][kWave];
+  const GridParams G = *gp;
+  const int n = *L_.n_slow;
+  const int lane = threadIdx.x & (kWave - 1);
+  const int wave = (int)((blockIdx.x * blockDim.x + threadIdx.x) / kWave);
+  const int nwaves = (int)(gridDim.x * blockDim.x / kWave);
+  const int gmax = max((G.g[0] + G.sx - 1) / G.sx, max(G.g[1], G.g[2]));
+  for (int e = wave; e < n; e += nwaves) {
+    const PRec Q = qsort[L_.slow_q[e]];
+    const size_t q = (size_t)Q.idx;
+    double thr = L_.slow_thr[e];
+    const double qv[3] = {Q.x, Q.y, Q.z};
+    const int c[3] = {cell_axis(qv[0], G, 0), cell_axis(qv[1], G, 1), cell_axis(qv[2], G, 2)};
+    double kd[K], md[K];
+    int ki[K], mi[K];
+#pragma unroll
+    for (int s = 0; s < K; ++s) {
+      kd[s] = INFINITY;
+      ki[s] = -1;
+    }
+    // cube radius: everything outside cube R is at least L_R away
+    int R = -1;
+    if (thr < INFINITY) {
+      for (int r = 1; r <= kSlowMaxR; ++r) {
+        const double L = block_reach(G, qv, c, r);
+        const double Lg = L - 2.0 * G.delta;
+        if (L == INFINITY || (Lg > 0.0 && thr < Lg * Lg)) {
+          R = r;
+          break;
+        }
+      }
+    }
+    if (R > 0) {
+      const int xl = max(c[0] - R * G.sx, 0), xh = min(c[0] + R * G.sx, G.g[0] - 1);
+      const int yl = max(c[1] - R, 0), yh = min(c[1] + R, G.g[1] - 1);
+      const int zl = max(c[2] - R, 0), zh = min(c[2] + R, G.g[2] - 1);
+      const int ny = yh - yl + 1, nrows = ny * (zh - zl + 1);  // <= 49
+      int cnt = 0, b = 0;
+      if (lane < nrows) {
+        const int y = yl + lane % ny, z = zl + lane / ny;
+        if (!(box_d2(G, qv, xl, xh, y, y, z, z) > thr)) {
+          const int row = (z * G.g[1] + y) * G.g[0];
+          b = start[row + xl];
+          cnt = start[row + xh + 1] - b;
+        }
+      }
+      int pre = cnt;  // inclusive wave scan of the row counts
+#pragma unroll
+      for (int o = 1; o < kWave; o <<= 1) {
+        const int t = __shfl_up(pre, o, kWave);
+        if (lane >= o) pre += t;
+      }
+      const int total = __shfl(pre, kWave - 1, kWave);
+      pre -= cnt;  // exclusive
+      for (int j0 = 0; j0 < total; j0 += kWave) {
+        const int j = j0 + lane;
+        // row of flattened record j: the last row whose prefix is <= j
+        int lo = 0;
+#pragma unroll
+        for (int step = 32; step > 0; step >>= 1) {
+          const int cand = lo + step;
+          const int pc = __shfl(pre, cand < nrows ? cand : 0, kWave);
+          if (cand < nrows && pc <= j) lo = cand;
+        }
+        const int pb = __shfl(b, lo, kWave), pp = __shfl(pre, lo, kWave);
+        if (j < total) knn_visit<K>(tsort[pb + (j - pp)], qv, thr, kd, ki);
+      }
+      // the lanes' survivors (usually ~K in all): compact them into LDS and
+      // rank each by counting smaller ones; more than 64 take the merge
+      int nsv = 0;
+#pragma unroll
+      for (int u = 0; u < K; ++u) nsv += kd[u] < INFINITY ? 1 : 0;
+      int off = nsv;
+#pragma unroll
+      for (int o = 1; o < kWave; o <<= 1) {
+        const int t = __shfl_up(off, o, kWave);
+        if (lane >= o) off += t;
+      }
+      const int tot = __shfl(off, kWave - 1, kWave);
+      off -= nsv;
+      if (tot <= kWave) {
+        double *bd = sd[threadIdx.x / kWave];
+        int *bi = si[threadIdx.x / kWave];
+#pragma unroll
+        for (int u = 0; u < K; ++u)
+          if (u < nsv) {
+            bd[off + u] = kd[u];
+            bi[off + u] = ki[u];
+          }
+        wave_sync_mem();
+        if (lane < tot) {
+          const double d = bd[lane];
+          const int id = bi[lane];
+          int rank = 0;
+          for (int t = 0; t < tot; ++t) rank += knn_less(bd[t], bi[t], d, id) ? 1 : 0;
+          if (rank < K) {
+            oidx[q * K + rank] = id;
+            odist[q * K + rank] = d;
+          }
+        }
+        if (lane >= tot && lane < K) {  // fewer than K survivors: empty slots
+          oidx[q * K + lane] = -1;
+          odist[q * K + lane] = INFINITY;
+        }
+        wave_sync_mem();  // the buffer is reused by this wave's next query
+        continue;
+      }
+      knn_wave_merge<K>(kd, ki, md, mi, lane);
+    }
+    for (int r = 0; R < 0 && r <= gmax; ++r) {
+      // the ring's cube clipped to the grid (a degenerate axis stays 1 thick);
+      // x reaches r * sx cells
+      const int xl = max(c[0] - r * G.sx, 0), xh = min(c[0] + r * G.sx, G.g[0] - 1);
+      const int yl = max(c[1] - r, 0), yh = min(c[1] + r, G.g[1] - 1);
+      const int zl = max(c[2] - r, 0), zh = min(c[2] + r, G.g[2] - 1);
+      const int bx = xh - xl + 1, by = yh - yl + 1, bz = zh - zl + 1;
+      const int nbox = bx * by * bz;
+      for (int u = lane; u < nbox; u += kWave) {
+        const int x = xl + u % bx, y = yl + (u / bx) % by, z = zl + u / (bx * by);
+        if (max((abs(x - c[0]) + G.sx - 1) / G.sx, max(abs(y - c[1]), abs(z - c[2]))) != r)
+          continue;
+        if (box_d2(G, qv, x, x, y, y, z, z) > thr) continue;
+        const int cell = (z * G.g[1] + y) * G.g[0] + x;
+        const int b = start[cell], en = start[cell + 1];
+        for (int t = b; t < en; ++t) knn_visit<K>(tsort[t], qv, thr, kd, ki);
+      }
+      knn_wave_merge<K>(kd, ki, md, mi, lane);
+      // lane 0 carries the merged list into the next ring
+#pragma unroll
+      for (int s = 0; s < K; ++s) {
+        kd[s] = lane == 0 ? md[s] : INFINITY;
+        ki[s] = lane == 0 ? mi[s] : -1;
+      }
+      if (md[K - 1] < INFINITY) thr = fmin(thr, md[K - 1] * md[K - 1] * (1.0 + 0x1p-46));
+      const double L = block_reach(G, qv, c, r);
+      if (L == INFINITY) break;
+      const double Lg = L - 2.0 * G.delta;
+      if (Lg > 0.0 && thr < Lg * Lg) break;  // all points with dsq <= thr seen
+    }
+    if (lane == 0) {
+#pragma unroll
+      for (int s = 0; s < K; ++s) {
+        oidx[q * K + s] = mi[s];
+        odist[q * K + s] = md[s];
+      }
+    }
+  }
+}
+
+// counters of the last call: [n_unstaged, n_slow, pad, pad]
+long long read_counter(navgpu_ctx *ctx, int which) {
+  if (!ctx) return -1;
+  auto it = ctx->bufs.find(kStats);
+  if (it == ctx->bufs.end() || !it->second.first) return -1;
+  int v[2] = {0, 0};
+  if (hipStreamSynchronize(ctx->stream) != hipSuccess) return -1;
+  if (hipMemcpy(v, it->second.first, 8, hipMemcpyDeviceToHost) != hipSuccess) return -1;
+  return (long long)v[which];
+}
+
+}  // namespace
+
+// ============================================================ host
+namespace nv {
+int knn_stamps_take(unsigned long long *out16) {
+#ifdef NAVGPU_STAMPS
+  HIP_TRY(hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_stamps), 16 * 8));
+  unsigned long long z[16] = {0};
+  HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), z, 16 * 8));
+  return NAVGPU_OK;
+#else
+  (void)out16;
+  return NAVGPU_EINVAL;
+#endif
+}
+}  // namespace nv
+
+// The k-NN call (navgpu_knn_dev): index build, query pass, slow pass; all on
+// the context's stream, nothing allocated once the workspace is warm.
+static int knn_run(navgpu_ctx *ctx, const double *tgt, size_t nt, const double *queries,
+                   size_t nq, int k, int32_t *idx, double *dist) {
+  ARG_CHECK(ctx && k >= 1 && k <= 16);
+  ARG_CHECK(nt < (size_t)INT32_MAX / 2 && nq < (size_t)INT32_MAX / 2);
+  if (!nq) return NAVGPU_OK;
+  ARG_CHECK(queries && idx && dist && (tgt || nt == 0));
+  const double occ = ctx->knn_occ;
+  const int sx = ctx->knn_sx;
+  const long long capl = (long long)((double)nt / occ) * 2 * sx + 1024;
+  ARG_CHECK(capl < INT32_MAX / 2);
+  const int cap = (int)capl;
+  const int nscan = cap + 1;  // start[] has one entry past the last cell
+  // binning geometry (k_bin_*): coarse buckets of 2^shift cells, at most
+  // kBinMaxBuckets of them, at least one cell per fine-pass thread
+  int shift = kBinMinShift;
+  while ((1 << shift) < kBinFineThreads) ++shift;
+  while (((long long)nscan + (1 << shift) - 1) >> shift > kBinMaxBuckets) ++shift;
+  if (shift > kBinMaxShift) {
+    set_err("knn: %zu targets exceed the binning capacity", nt);
+    return NAVGPU_ERANGE;
+  }
+  BinJob J;
+  J.shift = shift;
+  J.nb = (int)(((long long)nscan + (1 << shift) - 1) >> shift);
+  const size_t ns[2] = {nt, nq};
+  long long ntab = 0;
+  for (int side = 0; side < 2; ++side) {
+    BinSide &S = J.s[side];
+    S.n = (int)ns[side];
+    S.P = (int)std::max<size_t>(kBinP, (ns[side] / 2000 + 256) / 256 * 256);
+    S.nblk = (int)std::max<size_t>(1, (ns[side] + S.P - 1) / S.P);
+    S.tab = (int)ntab;
+    S.sub = side ? (int)nt : 0;
+    ntab += (long long)J.nb * S.nblk + 1;
+  }
+  const int nbs = (int)((ntab + kScanTile - 1) / kScanTile);
+  if (nbs > kScanTile) {
+    set_err("knn: binning table of %lld entries exceeds the scan capacity", ntab);
+    return NAVGPU_ERANGE;
+  }
+  const int nparts = (int)std::min<size_t>(kBBoxBlocks, std::max<size_t>(1, grid1d(nt, 256)));
+  double *part;
+  GridParams *gp;
+  int *tab, *offs, *tstart, *qstart, *bsum, *counters;
+  BinPt *bin_t = nullptr, *bin_q;
+  PRec *tsort = nullptr, *qsort;
+  RC(ws(ctx, kBBox, (size_t)kBBoxBlocks * 6, &part));
+  RC(ws(ctx, kParams, 1, &gp));
+  RC(ws(ctx, kCnt, (size_t)ntab, &tab));
+  RC(ws(ctx, kCellId, (size_t)ntab, &offs));
+  RC(ws(ctx, kStart, nscan, &tstart));
+  RC(ws(ctx, kQStart, nscan, &qstart));
+  RC(ws(ctx, kBSum, nbs, &bsum));
+  RC(ws(ctx, kStats, 4, &counters));  // zeroed by k_grid_params
+  if (nt) {
+    RC(ws(ctx, kSlotBuf, nt, &bin_t));
+    RC(ws(ctx, kTSort, nt, &tsort));
+  }
+  RC(ws(ctx, kQCell, nq, &bin_q));
+  RC(ws(ctx, kQSort, nq, &qsort));
+  J.s[0].p = tgt;
+  J.s[1].p = queries;
+  J.s[0].start = tstart;
+  J.s[1].start = qstart;
+  J.s[0].bin = bin_t;
+  J.s[1].bin = bin_q;
+  J.s[0].sorted = tsort;
+  J.s[1].sorted = qsort;
+  hipStream_t s = ctx->stream;
+  {
+    TimedRegion tb(ctx, "knn_build");
+    if (nt) {
+      hipLaunchKernelGGL(k_bbox_partial, dim3(nparts), dim3(256), 0, s, tgt, nt, part);
+      CHECK_LAUNCH("k_bbox_partial");
+    }
+    hipLaunchKernelGGL(k_grid_params, dim3(1), dim3(256), 0, s, part, nt ? nparts : 0, nt, cap,
+                       occ, sx, nq, gp, counters);
+    CHECK_LAUNCH("k_grid_params");
+    const dim3 gb(J.s[0].nblk + J.s[1].nblk);
+    hipLaunchKernelGGL(k_bin_hist, gb, dim3(256), 0, s, J, gp, tab);
+    CHECK_LAUNCH("k_bin_hist");
+    const int ntabi = (int)ntab;
+    hipLaunchKernelGGL(k_scan_sums, dim3(nbs), dim3(kScanBlock), 0, s, tab, ntabi, bsum);
+    CHECK_LAUNCH("k_scan_sums");
+    hipLaunchKernelGGL(k_scan_apply, dim3(nbs), dim3(kScanBlock), 0, s, tab, ntabi, bsum, offs);
+    CHECK_LAUNCH("k_scan_apply");
+    hipLaunchKernelGGL(k_bin_scatter, gb, dim3(256), 0, s, J, gp, (const int *)offs);
+    CHECK_LAUNCH("k_bin_scatter");
+    const size_t lds = (size_t)4 << shift;
+    if (lds > 48 * 1024)
+      HIP_TRY(hipFuncSetAttribute((const void *)k_bin_fine,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    hipLaunchKernelGGL(k_bin_fine, dim3(2 * J.nb), dim3(kBinFineThreads), lds, s, J, gp,
+                       (const int *)offs, nscan);
+    CHECK_LAUNCH("k_bin_fine");
+  }
+  KnnLists lists;
+  RC(ws(ctx, kSlowQ, nq, &lists.slow_q));
+  RC(ws(ctx, kSlowThr, nq, &lists.slow_thr));
+  lists.n_unstaged = counters;
+  lists.n_slow = counters + 1;
+  lists.vec_out = ((uintptr_t)idx % 16 == 0 && (uintptr_t)dist % 16 == 0) ? 1 : 0;
+  TimedRegion tr(ctx, "knn_query");
+  // tiles are walked by a grid of 8 x nbx blocks (block b -> XCD b % 8, the
+  // placement HW_REG_XCC_ID reports); more blocks than resident slots
+  // balance the uneven tiles
+  const int nbx = ctx->knn_blocks > 0
+                      ? ctx->knn_blocks
+                      : (int)std::min<size_t>(768, std::max<size_t>(1, nq / 1300 + 1));
+  const dim3 g(8 * nbx), b(kTileThreads);
+  const dim3 gs(std::max<unsigned>(1, std::min<unsigned>(2048, grid1d(nq, 256))));
+  const float lambda = (float)ctx->knn_lambda;
+#define KNN_CASE(KK)                                                                        \
+  case KK:                                                                                  \
+    hipLaunchKernelGGL((k_knn<KK>), g, b, 0, s, gp, tstart, tsort, qstart, qsort, idx, dist, \
+                       lists, lambda);                                                      \
+    hipLaunchKernelGGL((k_knn_slow<KK>), gs, dim3(256), 0, s, gp, tstart, tsort, qsort, idx, \
+                       dist, lists);                                                        \
+    break;
+  switch (k) {
+    KNN_CASE(1)
+    KNN_CASE(2)
+    KNN_CASE(3)
+    KNN_CASE(4)
+    KNN_CASE(5)
+    KNN_CASE(6)
+    KNN_CASE(7)
+    KNN_CASE(8)
+    KNN_CASE(9)
+    KNN_CASE(10)
+    KNN_CASE(11)
+    KNN_CASE(12)
+    KNN_CASE(13)
+    KNN_CASE(14)
+    KNN_CASE(15)
+    KNN_CASE(16)
+  }
+#undef KNN_CASE
+  CHECK_LAUNCH("k_knn");
+  return NAVGPU_OK;
+}
+
+extern "C" {
+
+int navgpu_knn_dev(navgpu_ctx *ctx, const double *tgt, size_t nt, const double *queries,
+                   size_t nq, int k, int32_t *idx, double *dist) {
+  return knn_run(ctx, tgt, nt, queries, nq, k, idx, dist);
+}
+
+int navgpu_knn_host(navgpu_ctx *ctx, const double *tgt, size_t nt, const double *queries,
+                    size_t nq, int k, int32_t *idx, double *dist) {
+  ARG_CHECK(ctx && k >= 1 && k <= 16);
+  if (!nq) return NAVGPU_OK;
+  ARG_CHECK(queries && idx && dist && (tgt || nt == 0));
+  double *dt = nullptr, *dq, *dd;
+  int32_t *di;
+  if (nt) RC(ws(ctx, kH0, 3 * nt, &dt));
+  RC(ws(ctx, kH1, 3 * nq, &dq));
+  RC(ws(ctx, kH2, nq * k, &di));
+  RC(ws(ctx, kH3, nq * k, &dd));
+  if (nt) HIP_TRY(hipMemcpyAsync(dt, tgt, 24 * nt, hipMemcpyHostToDevice, ctx->stream));
+  HIP_TRY(hipMemcpyAsync(dq, queries, 24 * nq, hipMemcpyHostToDevice, ctx->stream));
+  RC(navgpu_knn_dev(ctx, dt, nt, dq, nq, k, di, dd));
+  HIP_TRY(hipMemcpyAsync(idx, di, 4 * nq * k, hipMemcpyDeviceToHost, ctx->stream));
+  HIP_TRY(hipMemcpyAsync(dist, dd, 8 * nq * k, hipMemcpyDeviceToHost, ctx->stream));
+  HIP_TRY(hipStreamSynchronize(ctx->stream));
+  return NAVGPU_OK;
+}
+
+int navgpu_pair_knn_dev(navgpu_ctx *ctx, const double *src, const double *tgt, int R, int C,
+                        int k, int32_t *src_mask, int32_t *tgt_mask, int32_t *idx,
+                        double *dist) {
+  ARG_CHECK(ctx && R >= 0 && C >= 0);
+  const size_t N = (size_t)R * C;
+  if (!N) return NAVGPU_OK;
+  ARG_CHECK(src && tgt);
+  if (!src_mask && !tgt_mask) return navgpu_knn_dev(ctx, tgt, N, src, N, k, idx, dist);
+  // One curvature launch over both clouds, on a side stream forked from and
+  // joined back into the context's stream: it is f64-bound and independent
+  // of the (latency-bound) index build and query, so the two overlap.
+  RC(ensure_aux(ctx));
+  HIP_TRY(hipEventRecord(ctx->ev_fork, ctx->stream));
+  HIP_TRY(hipStreamWaitEvent(ctx->aux, ctx->ev_fork, 0));
+  {
+    TimedRegion tr(ctx, "curvature", ctx->aux);
+    if (src_mask && tgt_mask)
+      RC(launch_curvature(src, src_mask, nullptr, tgt, tgt_mask, nullptr, R, C, ctx->aux));
+    else if (src_mask)
+      RC(launch_curvature(src, src_mask, nullptr, nullptr, nullptr, nullptr, R, C, ctx->aux));
+    else
+      RC(launch_curvature(tgt, tgt_mask, nullptr, nullptr, nullptr, nullptr, R, C, ctx->aux));
+  }
+  HIP_TRY(hipEventRecord(ctx->ev_join, ctx->aux));
+  const int rc = knn_run(ctx, tgt, N, src, N, k, idx, dist);
+  HIP_TRY(hipStreamWaitEvent(ctx->stream, ctx->ev_join, 0));  // join before returning
+  return rc;
+}
+
+long long navgpu_knn_fallbacks(navgpu_ctx *ctx) { return read_counter(ctx, 1); }
+
+long long navgpu_knn_overflows(navgpu_ctx *ctx) { return read_counter(ctx, 0); }
+
+}  // extern "C"

@@ -14,37 +14,27 @@
 //                    feature queries against it, one workgroup per row
 //   k_rows_build / k_rows_query  the same split in two (slam.c keeps the
 //                    target trees across frames)
-//   k_bbox_partial, k_grid_params, k_bin_hist, k_scan_*, k_bin_scatter,
-//   k_bin_fine       global mode index: uniform grid over the target cloud,
-//                    both clouds counting-sorted by cell without global atomics
-//   k_knn<K>, k_knn_slow<K>
-//                    exact k-NN over that grid, (distance, index) ordering
-#include <hip/hip_runtime.h>
+//   (global mode: the grid index and exact k-NN live in knn.hip)
+#include "navgpu_common.h"
 
-#include <type_traits>
+#define NAVGPU_VERSION "navgpu 0.2 (gfx950)"
 
-#include <math.h>
-#include <stdarg.h>
-#include <stdint.h>
-#include <stdio.h>
-#include <stdlib.h>
-#include <string.h>
+namespace nv {
+char g_err[1024] = "";
 
-#include <algorithm>
-#include <map>
-#include <string>
-#include <utility>
-#include <vector>
+void set_err(const char *fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof(g_err), fmt, ap);
+  va_end(ap);
+}
+}  // namespace nv
 
-#include "navgpu.h"
-
-#pragma clang fp contract(off)
-
-#define NAVGPU_VERSION "navgpu 0.1 (gfx950)"
+using namespace nv;
 
 namespace {
 
-constexpr int kWave = 64;
+
 constexpr int kRowsBlock = 512;     // 8 waves per row workgroup
 #ifndef NAVGPU_ROWS_BUILD_BLOCK
 #define NAVGPU_ROWS_BUILD_BLOCK 512
@@ -55,69 +45,8 @@ constexpr int kMaxRowCols = 8191;   // 13-bit stack-entry fields
 constexpr int kCurvTile = 256;
 
 // Diagnostic phase stamps (build with -DNAVGPU_STAMPS; never in the product
-// build): lane 0 of each wave adds s_memtime deltas per phase into g_stamps.
-#ifdef NAVGPU_STAMPS
-__device__ unsigned long long g_stamps[16];
-#define NV_STAMP(v) const unsigned long long v = __builtin_amdgcn_s_memtime()
-#define NV_STAMP_ADD(slot, a, b) \
-  if ((threadIdx.x & 63) == 0) atomicAdd(&g_stamps[slot], (b) - (a))
-#define NV_STAMP_ADD0(slot, a, b) \
-  if (threadIdx.x == 0) atomicAdd(&g_stamps[slot], (b) - (a))
-#define NV_COUNT0(slot) \
-  if (threadIdx.x == 0) atomicAdd(&g_stamps[slot], 1ull)
-#else
-#define NV_COUNT0(slot)
-#define NV_STAMP(v)
-#define NV_STAMP_ADD(slot, a, b)
-#define NV_STAMP_ADD0(slot, a, b)
-#endif
-
-// ------------------------------------------------------------------ errors
-char g_err[1024] = "";
-
-void set_err(const char *fmt, ...) {
-  va_list ap;
-  va_start(ap, fmt);
-  vsnprintf(g_err, sizeof(g_err), fmt, ap);
-  va_end(ap);
-}
-
-#define HIP_TRY(expr)                                                          \
-  do {                                                                         \
-    hipError_t e_ = (expr);                                                    \
-    if (e_ != hipSuccess) {                                                    \
-      set_err("%s:%d %s: %s", __FILE__, __LINE__, #expr,                      \
-              hipGetErrorString(e_));                                          \
-      return NAVGPU_EHIP;                                                      \
-    }                                                                          \
-  } while (0)
-
-#define CHECK_LAUNCH(name)                                                     \
-  do {                                                                         \
-    hipError_t e_ = hipGetLastError();                                         \
-    if (e_ != hipSuccess) {                                                    \
-      set_err("launch %s: %s", name, hipGetErrorString(e_));                  \
-      return NAVGPU_EHIP;                                                      \
-    }                                                                          \
-  } while (0)
-
-#define ARG_CHECK(cond)                                                        \
-  do {                                                                         \
-    if (!(cond)) {                                                             \
-      set_err("invalid argument: %s", #cond);                                 \
-      return NAVGPU_EINVAL;                                                    \
-    }                                                                          \
-  } while (0)
-
 // ============================================================ device helpers
 
-// utils/kdtree.c:14-17 (euclideanDistance; gcc folds pow(v,2) to v*v) and
-// src/slam.c:28-33,47-50: sqrt((dx*dx + dy*dy) + dz*dz), no contraction.
-__device__ __forceinline__ double ref_dist(double ax, double ay, double az,
-                                           double bx, double by, double bz) {
-  const double dx = ax - bx, dy = ay - by, dz = az - bz;
-  return __builtin_sqrt(dx * dx + dy * dy + dz * dz);
-}
 
 // src/slam.c:15-58 for one point with its four same-row neighbours
 // (k = -2, -1, +1, +2 in that order). The four distances are computed once
@@ -166,47 +95,6 @@ __device__ __forceinline__ void block_copy(double *dst, const double *src,
   for (int i = threadIdx.x; i < n; i += blockDim.x) dst[i] = src[i];
 }
 
-__device__ __forceinline__ int lanes_below(unsigned long long bal) {
-  return __builtin_amdgcn_mbcnt_hi((unsigned)(bal >> 32),
-                                   __builtin_amdgcn_mbcnt_lo((unsigned)bal, 0u));
-}
-
-__device__ __forceinline__ void wave_sync_mem() {
-  // Cross-lane hand-off through memory inside one wavefront (LDS, or global
-  // scratch of the large-n build): workgroup-scope release/acquire makes the
-  // other lanes' stores visible; wave_barrier stops code motion across it.
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-}
-
-// Block-wide exclusive scan of one int per thread. scratch: >= nwaves+1 ints.
-__device__ int block_excl_scan(int v, int *scratch, int *total) {
-  const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
-  const int nw = blockDim.x / kWave;
-  int incl = v;
-#pragma unroll
-  for (int o = 1; o < kWave; o <<= 1) {
-    int t = __shfl_up(incl, o, kWave);
-    if (lane >= o) incl += t;
-  }
-  if (lane == kWave - 1) scratch[wid] = incl;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    int acc = 0;
-    for (int w = 0; w < nw; ++w) {
-      int t = scratch[w];
-      scratch[w] = acc;
-      acc += t;
-    }
-    scratch[nw] = acc;
-  }
-  __syncthreads();
-  const int res = scratch[wid] + incl - v;
-  *total = scratch[nw];
-  __syncthreads();
-  return res;
-}
 
 // Stable compaction of [0, C): flag(j) -> write(j, rank). Each thread owns a
 // contiguous chunk so ranks follow column order (flattenPoints order,
@@ -2122,1383 +2010,10 @@ __global__ __launch_bounds__(256) void k_corr_pack(const double *__restrict__ en
   }
 }
 
-// ============================================================ global mode
-// Uniform grid over the target cloud. Cells are numbered x-fastest, so the
-// cells x-1..x+1 of one (y,z) row are contiguous in the cell-sorted target
-// array: a query's 3x3x3 neighbourhood is 9 contiguous "runs".
-struct GridParams {
-  double o[3];      // origin = target bbox min
-  double e[3], inv_e[3];  // cell edge per axis: x h / sx, y and z h
-  double h;         // the coarse edge
-  double delta;     // slack on cell boxes (cell assignment is f64 arithmetic)
-  double emax;      // largest bbox extent
-  int g[3];
-  int ncells;
-  int sx;           // x cells per h: a query's block is cells x-sx .. x+sx,
-                    // y-1 .. y+1, z-1 .. z+1 (the reach is >= h on every axis)
-  int tile_w;       // cells per k_knn tile along x
-};
-
-// soff entries per staged row of a k_knn tile (W + 2 sx + 1 <= kTileCols)
-#ifndef NAVGPU_TILE_COLS
-#define NAVGPU_TILE_COLS 136
-#endif
-constexpr int kTileCols = NAVGPU_TILE_COLS;
-constexpr int kMaxSx = 8;
-#ifndef NAVGPU_KNN_SX
-#define NAVGPU_KNN_SX 1  // sx = 2: query stage 183 -> 177 us, build 99 -> 109 us (K3)
-#endif
-#ifndef NAVGPU_TILE_QUERIES
-#define NAVGPU_TILE_QUERIES 165.0  // target queries per k_knn tile
-#endif
-#ifndef NAVGPU_TILE_REC
-#define NAVGPU_TILE_REC 1600
-#endif
-
-struct __align__(16) Rec16 {  // cell-sorted target: (coords - origin) in f32
-  float x, y, z;
-  int cx;  // x index of its grid cell (the f64 binning's, exact)
-};
-struct __align__(16) TRec {  // cell-sorted target, exact: the reference f64 point + its index
-  double x, y, z;
-  int idx, pad;
-};
-
-constexpr int kBBoxBlocks = 1024;
-constexpr int kKeyBits = 10;  // local id in the low bits of a key: run (4) | offset (6)
-constexpr uint32_t kKeyMask = (1u << kKeyBits) - 1;
-constexpr uint32_t kNoKey = 0xffffffffu;
-
-// per-block min/max of the finite coordinates -> part[block][6]
-__global__ __launch_bounds__(256) void k_bbox_partial(const double *__restrict__ p,
-                                                      size_t n, double *__restrict__ part) {
-  __shared__ double s[4][6];
-  double v6[6] = {INFINITY, INFINITY, INFINITY, -INFINITY, -INFINITY, -INFINITY};
-  // batches of 4 points per thread, all loads of a batch in flight together
-  // (flat 16-B loads of the 3n doubles measured the same, r2)
-  constexpr int U = 4;
-  const size_t stride = (size_t)gridDim.x * blockDim.x;
-  for (size_t ib = (size_t)blockIdx.x * blockDim.x + threadIdx.x; ib < n; ib += U * stride) {
-    double v[U][3];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const size_t i = ib + u * stride;
-#pragma unroll
-      for (int a = 0; a < 3; ++a) v[u][a] = i < n ? p[3 * i + a] : INFINITY;
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u)
-#pragma unroll
-      for (int a = 0; a < 3; ++a)
-        if (fabs(v[u][a]) < INFINITY) {
-          v6[a] = fmin(v6[a], v[u][a]);
-          v6[3 + a] = fmax(v6[3 + a], v[u][a]);
-        }
-  }
-#pragma unroll
-  for (int a = 0; a < 3; ++a)
-    for (int o = kWave / 2; o > 0; o >>= 1) {
-      v6[a] = fmin(v6[a], __shfl_xor(v6[a], o, kWave));
-      v6[3 + a] = fmax(v6[3 + a], __shfl_xor(v6[3 + a], o, kWave));
-    }
-  const int wid = threadIdx.x / kWave;
-  if ((threadIdx.x & (kWave - 1)) == 0)
-    for (int a = 0; a < 6; ++a) s[wid][a] = v6[a];
-  __syncthreads();
-  if (threadIdx.x < 6) {
-    const int a = threadIdx.x;
-    double r = s[0][a];
-    for (int w = 1; w < 4; ++w) r = a < 3 ? fmin(r, s[w][a]) : fmax(r, s[w][a]);
-    part[blockIdx.x * 6 + a] = r;
-  }
-}
-
-// bbox from the partials, then the grid: h for ~occ points per cell, capped
-// at `cap` cells.
-__global__ __launch_bounds__(256) void k_grid_params(const double *__restrict__ part,
-                                                     int nparts, size_t n, int cap,
-                                                     double occ, int sx, size_t nq,
-                                                     GridParams *gp, int *counters) {
-  // also resets the call's k-NN counters (overflow tiles, slow queries): one
-  // launch fewer than a memset
-  if (threadIdx.x < 4) counters[threadIdx.x] = 0;
-  __shared__ double s[4][6];
-  double v6[6] = {INFINITY, INFINITY, INFINITY, -INFINITY, -INFINITY, -INFINITY};
-  for (int b = threadIdx.x; b < nparts; b += blockDim.x)
-    for (int a = 0; a < 6; ++a)
-      v6[a] = a < 3 ? fmin(v6[a], part[b * 6 + a]) : fmax(v6[a], part[b * 6 + a]);
-#pragma unroll
-  for (int a = 0; a < 3; ++a)
-    for (int o = kWave / 2; o > 0; o >>= 1) {
-      v6[a] = fmin(v6[a], __shfl_xor(v6[a], o, kWave));
-      v6[3 + a] = fmax(v6[3 + a], __shfl_xor(v6[3 + a], o, kWave));
-    }
-  if ((threadIdx.x & (kWave - 1)) == 0)
-    for (int a = 0; a < 6; ++a) s[threadIdx.x / kWave][a] = v6[a];
-  __syncthreads();
-  if (threadIdx.x != 0) return;
-  for (int w = 1; w < (int)blockDim.x / kWave; ++w)
-    for (int a = 0; a < 6; ++a)
-      v6[a] = a < 3 ? fmin(v6[a], s[w][a]) : fmax(v6[a], s[w][a]);
-  GridParams G;
-  double lo[3], ext[3];
-  bool any = n > 0;
-  for (int a = 0; a < 3; ++a) {
-    if (!(v6[a] <= v6[3 + a])) any = false;
-    lo[a] = v6[a];
-    ext[a] = v6[3 + a] - v6[a];
-  }
-  if (!any) {
-    for (int a = 0; a < 3; ++a) {
-      G.o[a] = 0.0;
-      G.g[a] = 1;
-      G.e[a] = G.inv_e[a] = 1.0;
-    }
-    G.h = G.delta = 1.0;
-    G.sx = 1;
-    G.emax = 0.0;
-    G.ncells = 1;
-    G.tile_w = 1;
-    *gp = G;
-    return;
-  }
-  const double emax = fmax(ext[0], fmax(ext[1], ext[2]));
-  const double floor_e = fmax(emax * 1e-3, 1e-9);
-  double vol = 1.0;
-  for (int a = 0; a < 3; ++a) vol *= fmax(ext[a], floor_e);
-  double h = cbrt(vol * occ / (double)n);
-  if (!(h > 0) || !(h < INFINITY)) h = fmax(emax, 1.0);
-  int g[3];
-  for (int it = 0; it < 200; ++it) {
-    long long tot = 1;
-    for (int a = 0; a < 3; ++a) {
-      const double ea = a == 0 ? h / sx : h;
-      double ga = floor(ext[a] / ea) + 1.0;  // covers [lo, lo + ext] inclusive
-      if (ga > 2048) ga = 2048;
-      g[a] = (int)ga;
-      tot *= g[a];
-    }
-    if (tot <= cap) break;
-    h *= 1.1;
-  }
-  for (int a = 0; a < 3; ++a) G.o[a] = lo[a];
-  G.h = h;
-  G.sx = sx;
-  for (int a = 0; a < 3; ++a) {
-    G.e[a] = a == 0 ? h / sx : h;
-    G.inv_e[a] = 1.0 / G.e[a];
-  }
-  G.delta = 1e-7 * (emax + h);
-  G.emax = emax;
-  G.g[0] = g[0];
-  G.g[1] = g[1];
-  G.g[2] = g[2];
-  G.ncells = g[0] * g[1] * g[2];
-  // tile width: ~165 queries per 192-thread tile, and its 9 staged row
-  // segments of W + 2 sx cells within ~90 % of the LDS record budget
-  const double occ_q = (double)nq / G.ncells, occ_t = (double)n / G.ncells;
-  double w = fmin(NAVGPU_TILE_QUERIES / fmax(occ_q, 1e-9),
-                  0.9 * NAVGPU_TILE_REC / (9.0 * fmax(occ_t, 1e-9)) - 2.0 * sx);
-  // balanced: the fewest tiles per grid row at that width, then equal widths
-  // (a ragged last tile would pay a full staging + barrier cycle for a few
-  // cells)
-  const int wmax = (int)fmax(1.0, fmin((double)(kTileCols - 1 - 2 * sx), floor(w)));
-  const int tpr = (G.g[0] + wmax - 1) / wmax;
-  G.tile_w = (G.g[0] + tpr - 1) / tpr;
-  *gp = G;
-}
-
-__device__ __forceinline__ int cell_axis(double v, const GridParams &G, int a) {
-  const double t = (v - G.o[a]) * G.inv_e[a];
-  if (!(t >= 0.0)) return 0;  // below the grid, or NaN
-  if (t >= (double)G.g[a]) return G.g[a] - 1;
-  return (int)t;
-}
-
-__device__ __forceinline__ int cell_of(const double *p, const GridParams &G) {
-  return (cell_axis(p[2], G, 2) * G.g[1] + cell_axis(p[1], G, 1)) * G.g[0] +
-         cell_axis(p[0], G, 0);
-}
-
-constexpr int kScanBlock = 1024, kScanPer = 4,
-              kScanTile = kScanBlock * kScanPer;
-
-__global__ __launch_bounds__(kScanBlock) void k_scan_sums(
-    const int *__restrict__ in, int n, int *__restrict__ bsum) {
-  __shared__ int scratch[40];
-  const int base = blockIdx.x * kScanTile + threadIdx.x * kScanPer;
-  int s = 0;
-#pragma unroll
-  for (int k = 0; k < kScanPer; ++k)
-    if (base + k < n) s += in[base + k];
-  int total;
-  block_excl_scan(s, scratch, &total);
-  if (threadIdx.x == 0) bsum[blockIdx.x] = total;
-}
-
-__global__ __launch_bounds__(kScanBlock) void k_scan_apply(
-    const int *__restrict__ in, int n, const int *__restrict__ bsum,
-    int *__restrict__ out) {
-  __shared__ int scratch[40];
-  const int base = blockIdx.x * kScanTile + threadIdx.x * kScanPer;
-  int v[kScanPer];
-  int s = 0;
-#pragma unroll
-  for (int k = 0; k < kScanPer; ++k) {
-    v[k] = base + k < n ? in[base + k] : 0;
-    s += v[k];
-  }
-  // this block's offset: the sum of the block totals before it, read straight
-  // from bsum (at most kScanTile of them; a separate top-level scan launch
-  // costs more than these few reads)
-  int pre = 0;
-  for (int i = threadIdx.x; i < (int)blockIdx.x; i += blockDim.x) pre += bsum[i];
-  int total, ptot;
-  block_excl_scan(pre, scratch, &ptot);
-  __syncthreads();  // scratch is reused by the next scan
-  int off = block_excl_scan(s, scratch, &total) + ptot;
-#pragma unroll
-  for (int k = 0; k < kScanPer; ++k) {
-    if (base + k < n) out[base + k] = off;
-    off += v[k];
-  }
-}
-
-// ---- cell binning: counting sort of both clouds by grid cell --------------
-// Scattered global atomics run at the memory side on this part (~24 G/s
-// whatever their scope), so the sort uses none: LDS histograms and LDS ranks
-// only.
-//  k_bin_hist    each block takes a contiguous chunk of points and counts
-//                their coarse bucket (cell >> shift) in LDS; counts land in a
-//                bucket-major table[b * nblk + block], so ONE exclusive scan
-//                of the table gives every (bucket, block) its output offset.
-//  k_bin_scatter same chunks: each point gets an LDS rank within its
-//                (bucket, block) and moves to the coarse-bucketed array.
-//  k_bin_fine    one block per bucket: LDS counting sort over the bucket's
-//                2^shift cells, writes start[] for them and every point at its
-//                final cell-sorted position (target: Rec16 + TRec;
-//                query: its index). Order inside a cell is unspecified: the
-//                k-NN result does not depend on it (ties are resolved by
-//                (distance, index) in the exact stage).
-// Side 0 = targets, side 1 = queries; both are handled by the same launches
-// (block ranges), and their tables are concatenated so one scan covers both.
-struct BinPt {
-  double x, y, z;
-  int idx, cell;
-};
-struct BinSide {
-  const double *p;
-  int n, P, nblk;
-  int tab;  // offset of this side's table in the concatenated table
-  int sub;  // subtracted from scanned offsets (targets' total, for side 1)
-  int *start;
-};
-struct BinJob {
-  BinSide s[2];
-  int shift, nb;  // buckets per side
-  BinPt *bin_t;
-  int2 *bin_q;    // (idx, cell)
-  Rec16 *rec;
-  TRec *tsort;
-  int *qperm;
-};
-constexpr int kBinMaxBuckets = 4096;
-constexpr int kBinMaxShift = 15;
-
-__device__ __forceinline__ int bin_side(const BinJob &J, int &blk) {
-  const int side = blk >= J.s[0].nblk ? 1 : 0;
-  if (side) blk -= J.s[0].nblk;
-  return side;
-}
-
-#ifndef NAVGPU_BIN_UNROLL
-#define NAVGPU_BIN_UNROLL 8
-#endif
-// points per thread with loads in flight (r2 sweep: 4 / 8 / 16 -> isolated
-// build 97 / 98 / 96 us, but the two-in-flight bench step 0.2805 ms with 16
-// against 0.2767 with 8: the build shares the chip with a query stage there)
-constexpr int kBinUnroll = NAVGPU_BIN_UNROLL;
-
-struct P3 {
-  double x, y, z;
-};
-
-// the block's chunk in batches of kBinUnroll points per thread: every load of
-// a batch is issued before any of its cells is used, so a wave keeps
-// kBinUnroll x 24 B per lane in flight instead of one point's worth
-template <class F>
-__device__ __forceinline__ void bin_chunk(const BinSide &S, int blk, const GridParams &G, F f) {
-  const int i0 = blk * S.P, i1 = min(S.n, (blk + 1) * S.P);
-  const int bd = (int)blockDim.x;
-  for (int ib = i0; ib < i1; ib += kBinUnroll * bd) {
-    P3 v[kBinUnroll];
-#pragma unroll
-    for (int u = 0; u < kBinUnroll; ++u) {
-      const int i = ib + u * bd + (int)threadIdx.x;
-      if (i < i1) v[u] = *(const P3 *)(S.p + 3 * (size_t)i);
-    }
-#pragma unroll
-    for (int u = 0; u < kBinUnroll; ++u) {
-      const int i = ib + u * bd + (int)threadIdx.x;
-      if (i < i1) f(i, v[u], cell_of(&v[u].x, G));
-    }
-  }
-}
-
-__global__ __launch_bounds__(256) void k_bin_hist(BinJob J,
-                                                  const GridParams *__restrict__ gp,
-                                                  int *__restrict__ table) {
-  __shared__ int hist[kBinMaxBuckets];
-  int blk = blockIdx.x;
-  const BinSide S = J.s[bin_side(J, blk)];
-  const GridParams G = *gp;
-  for (int b = threadIdx.x; b < J.nb; b += blockDim.x) hist[b] = 0;
-  __syncthreads();
-  bin_chunk(S, blk, G, [&](int, const P3 &, int c) { atomicAdd(&hist[c >> J.shift], 1); });
-  __syncthreads();
-  for (int b = threadIdx.x; b < J.nb; b += blockDim.x)
-    table[S.tab + b * S.nblk + blk] = hist[b];
-  if (blk == 0 && threadIdx.x == 0) table[S.tab + J.nb * S.nblk] = 0;  // sentinel
-}
-
-__global__ __launch_bounds__(256) void k_bin_scatter(BinJob J,
-                                                     const GridParams *__restrict__ gp,
-                                                     const int *__restrict__ offs) {
-  __shared__ int cur[kBinMaxBuckets];
-  int blk = blockIdx.x;
-  const int side = bin_side(J, blk);
-  const BinSide S = J.s[side];
-  const GridParams G = *gp;
-  for (int b = threadIdx.x; b < J.nb; b += blockDim.x)
-    cur[b] = offs[S.tab + b * S.nblk + blk] - S.sub;
-  __syncthreads();
-  bin_chunk(S, blk, G, [&](int i, const P3 &v, int c) {
-    const int pos = atomicAdd(&cur[c >> J.shift], 1);
-    if (side == 0) {
-      BinPt t;
-      t.x = v.x;
-      t.y = v.y;
-      t.z = v.z;
-      t.idx = i;
-      t.cell = c;
-      J.bin_t[pos] = t;
-    } else {
-      J.bin_q[pos] = make_int2(i, c);
-    }
-  });
-}
-
-#ifndef NAVGPU_BIN_P
-#define NAVGPU_BIN_P 4096  // minimum points per k_bin_hist / k_bin_scatter block
-#endif
-#ifndef NAVGPU_BIN_FINE_THREADS
-#define NAVGPU_BIN_FINE_THREADS 512
-#endif
-#ifndef NAVGPU_BIN_MIN_SHIFT
-// coarse buckets of 2^10 cells (r2 two-in-flight bench A/B, two sessions of
-// 3 interleaved runs: 9 -> 0.2745 / 0.2744 ms, 10 -> 0.2716 / 0.2733, 11 ->
-// 0.2942; profiles/r2/bench_ab_r2l.txt)
-#define NAVGPU_BIN_MIN_SHIFT 10
-#endif
-constexpr int kBinFineThreads = NAVGPU_BIN_FINE_THREADS;
-
-constexpr int kBinFineHold = 4096 / kBinFineThreads;  // points per thread held in registers
-
-// One bucket: count its points per cell (LDS), scan, write the cell starts,
-// then place every point. The first kBinFineHold * blockDim points stay in
-// registers between the count and the placement (one global read, not two);
-// a larger bucket re-reads the rest.
-template <bool QSIDE>
-__device__ void bin_fine_bucket(const BinJob &J, const BinSide &S, const GridParams *gp,
-                                int lo, int hi, int base, int ncell, int nscan, int *cnt,
-                                int *scratch) {
-  typedef typename std::conditional<QSIDE, int2, BinPt>::type E;
-  const E *src = QSIDE ? (const E *)J.bin_q : (const E *)J.bin_t;
-  auto cell_of_e = [](const E &e) {
-    if constexpr (QSIDE) return e.y; else return e.cell;
-  };
-  for (int j = threadIdx.x; j < ncell; j += blockDim.x) cnt[j] = 0;
-  __syncthreads();
-  E hold[kBinFineHold];
-  const int bd = (int)blockDim.x, held_end = min(hi, lo + kBinFineHold * bd);
-#pragma unroll
-  for (int u = 0; u < kBinFineHold; ++u) {
-    const int i = lo + u * bd + (int)threadIdx.x;
-    if (i < held_end) hold[u] = src[i];
-  }
-#pragma unroll
-  for (int u = 0; u < kBinFineHold; ++u) {
-    const int i = lo + u * bd + (int)threadIdx.x;
-    if (i < held_end) atomicAdd(&cnt[cell_of_e(hold[u]) - base], 1);
-  }
-  for (int i = held_end + (int)threadIdx.x; i < hi; i += bd)
-    atomicAdd(&cnt[cell_of_e(src[i]) - base], 1);
-  __syncthreads();
-  // exclusive scan over the bucket's cells: each thread owns a contiguous run
-  const int per = ncell / bd;  // ncell is a multiple of the block size
-  const int j0 = (int)threadIdx.x * per;
-  int sum = 0;
-  for (int u = 0; u < per; ++u) sum += cnt[j0 + u];
-  int total;
-  int acc = lo + block_excl_scan(sum, scratch, &total);
-  for (int u = 0; u < per; ++u) {
-    const int v = cnt[j0 + u];
-    cnt[j0 + u] = acc;
-    if (base + j0 + u < nscan) S.start[base + j0 + u] = acc;
-    acc += v;
-  }
-  __syncthreads();
-  const GridParams G = *gp;
-  auto place = [&](const E &e) {
-    if constexpr (QSIDE) {
-      J.qperm[atomicAdd(&cnt[e.y - base], 1)] = e.x;
-    } else {
-      const int pos = atomicAdd(&cnt[e.cell - base], 1);
-      TRec t;
-      t.x = e.x;
-      t.y = e.y;
-      t.z = e.z;
-      t.idx = e.idx;
-      t.pad = 0;
-      J.tsort[pos] = t;
-      Rec16 r;
-      r.x = (float)(e.x - G.o[0]);
-      r.y = (float)(e.y - G.o[1]);
-      r.z = (float)(e.z - G.o[2]);
-      r.cx = e.cell % G.g[0];
-      J.rec[pos] = r;
-    }
-  };
-#pragma unroll
-  for (int u = 0; u < kBinFineHold; ++u) {
-    const int i = lo + u * bd + (int)threadIdx.x;
-    if (i < held_end) place(hold[u]);
-  }
-  for (int i = held_end + (int)threadIdx.x; i < hi; i += bd) place(src[i]);
-}
-
-__global__ __launch_bounds__(kBinFineThreads) void k_bin_fine(
-    BinJob J, const GridParams *__restrict__ gp, const int *__restrict__ offs,
-    int nscan) {
-  extern __shared__ int cnt[];  // 2^shift
-  __shared__ int scratch[40];
-  const int side = blockIdx.x >= J.nb ? 1 : 0;
-  const int b = blockIdx.x - (side ? J.nb : 0);
-  const BinSide S = J.s[side];
-  const int ncell = 1 << J.shift, base = b << J.shift;
-  const int lo = offs[S.tab + b * S.nblk] - S.sub;
-  const int hi = offs[S.tab + (b + 1) * S.nblk] - S.sub;
-  if (side)
-    bin_fine_bucket<true>(J, S, gp, lo, hi, base, ncell, nscan, cnt, scratch);
-  else
-    bin_fine_bucket<false>(J, S, gp, lo, hi, base, ncell, nscan, cnt, scratch);
-}
-
-// (d, i) < (kd, ki): distance first, then index. Never true for d = inf/NaN.
-__device__ __forceinline__ bool knn_less(double d, int i, double kd, int ki) {
-  return d < kd || (d == kd && i < ki);
-}
-
-// squared distance from q to the box of cells [x0..x1] x [y0..y1] x [z0..z1]
-// grown by delta: a lower bound on the reference dsq of any point binned there
-__device__ __forceinline__ double box_d2(const GridParams &G, const double *qv,
-                                         int x0, int x1, int y0, int y1, int z0,
-                                         int z1) {
-  const int lo[3] = {x0, y0, z0}, hi[3] = {x1, y1, z1};
-  double s = 0.0;
-#pragma unroll
-  for (int a = 0; a < 3; ++a) {
-    const double bl = G.o[a] + lo[a] * G.e[a] - G.delta;
-    const double bh = G.o[a] + (hi[a] + 1) * G.e[a] + G.delta;
-    // boundary cells also hold everything clamped into them
-    const double e = fmax(0.0, fmax(lo[a] > 0 ? bl - qv[a] : 0.0,
-                                     hi[a] < G.g[a] - 1 ? qv[a] - bh : 0.0));
-    s += e * e;
-  }
-  return s;
-}
-
-// Distance from q (in cell c) to the outside of its block of radius r: cells
-// x - r sx .. x + r sx, y - r .. y + r, z - r .. z + r. A block face on the
-// grid boundary does not count (the boundary cells hold everything clamped
-// into them); INFINITY when every face is.
-__device__ __forceinline__ double block_reach(const GridParams &G, const double *qv,
-                                              const int c[3], int r) {
-  double L = INFINITY;
-#pragma unroll
-  for (int a = 0; a < 3; ++a) {
-    const int ra = a == 0 ? r * G.sx : r;
-    if (c[a] - ra > 0) L = fmin(L, qv[a] - (G.o[a] + (c[a] - ra) * G.e[a]));
-    if (c[a] + ra < G.g[a] - 1) L = fmin(L, (G.o[a] + (c[a] + ra + 1) * G.e[a]) - qv[a]);
-  }
-  return L;
-}
-
-// f32 admission bound for an f64 dsq bound T: every candidate whose exact
-// dsq is <= T has an f32 dsq (coordinates relative to the grid origin, each
-// f32 difference within dl of the exact one) <= the returned value.
-__device__ __forceinline__ float f32_bound(double T, double dl) {
-  if (!(T < INFINITY)) return INFINITY;
-  const double E = T * 0x1p-20 + 4.0 * dl * __builtin_sqrt(T) + 4.0 * dl * dl;
-  return (float)((T + E) * (1.0 + 0x1p-20));
-}
-
-__device__ __forceinline__ uint32_t umed3(uint32_t a, uint32_t b, uint32_t c) {
-  return max(min(a, b), min(max(a, b), c));
-}
-
-// (dy, dz) of the 9 runs of a 3x3x3 neighbourhood: centre, faces, corners
-__device__ __forceinline__ void run_dydz(int r, int &dy, int &dz) {
-  dy = r == 0 ? 0 : (r == 1 ? -1 : (r == 2 ? 1 : (r <= 4 ? 0 : (r & 1 ? -1 : 1))));
-  dz = r <= 2 ? 0 : (r == 3 ? -1 : (r == 4 ? 1 : (r <= 6 ? -1 : 1)));
-}
-
-// One query of the global-mode k-NN.
-// Fast path over the query's 3x3x3 cell neighbourhood, taken as 9 runs: the
-// three cells x-1..x+1 of one (y, z) row are contiguous in the cell-sorted
-// arrays, so each run is one record range (own row first, then faces, then
-// corners). Each candidate gets an f32 distance (coordinates relative to the
-// grid origin) packed with its local id (run | offset) into a 32-bit key; a
-// sorted list of the K+1 smallest keys is kept by branch-free median-of-3
-// insertion. The K+1 survivors are then re-evaluated with the reference f64
-// formula and ordered by (distance, index); the result is certified exact when
-// every candidate left out (visited but not kept, or outside the block) is
-// provably farther than the K-th, using the f32 error bound. Otherwise (near
-// ties, a neighbourhood reaching past the block, overfull runs) the query is
-// queued for k_knn_slow with the K-th distance found as its starting bound.
-// runs(r, t0, t1, g0): record range [t0, t1) of run r in the index space of
-// the fetches and g0 = the global (cell-sorted) position of record t0.
-// pair(t): packed coordinates of records t, t+1 (t even); idx(p): index of
-// record p. A run is walked in even-aligned pairs from t0 & ~1, lanes outside
-// [t0, t1) masked, so the key's local id (run | position from t0 & ~1) is the
-// wave-uniform loop counter.
-constexpr int kRunOffBits = 6;  // candidates per run addressable by a key
-
-struct KnnLists {
-  int *ovf_tiles, *n_ovf;  // tiles whose segments overflow the LDS budget
-  int *slow_q, *n_slow;    // queries the fast path could not certify
-  double *slow_thr;        // their starting bound (K-th dsq upper bound)
-  int vec_out;             // outputs 16-B aligned: k_knn may store them as vectors
-};
-
-typedef float f2 __attribute__((ext_vector_type(2)));
-struct Pair3 {
-  f2 x, y, z;
-};
-// record cursors for knn_one: load() = packed coordinates of the current
-// pair of records, next() = the following pair
-// The k_knn LDS tile, pair-interleaved in two planes of 16 B per pair of
-// records: XY (x0 x1 y0 y1) and, kZgOff floats further, ZG (z0 z1 g0 g1).
-// A 16-B stride spreads the lanes' b128 reads over all bank quads (one 32-B
-// pair stride used only every other quad: a 2-way conflict floor).
-#ifndef NAVGPU_TILE_REC
-#define NAVGPU_TILE_REC 1600
-#endif
-constexpr int kTilePairs = NAVGPU_TILE_REC / 2 + 2;  // two spare pairs: read-ahead
-constexpr int kZgOff = 4 * kTilePairs;
-struct LdsPairCursor {
-  const float *p;  // XY plane, pair P at p = XY + 4 P
-  __device__ Pair3 load() const {
-    const float4 xy = *(const float4 *)p;
-    const float2 zz = *(const float2 *)(p + kZgOff);
-    Pair3 P;
-    P.x = f2{xy.x, xy.y};
-    P.y = f2{xy.z, xy.w};
-    P.z = f2{zz.x, zz.y};
-    return P;
-  }
-  __device__ void next() { p += 4; }
-};
-struct RecPairCursor {  // global Rec16 array (two records of padding at its end)
-  const Rec16 *p;
-  __device__ Pair3 load() const {
-    const Rec16 a = p[0], b = p[1];
-    Pair3 P;
-    P.x = f2{a.x, b.x};
-    P.y = f2{a.y, b.y};
-    P.z = f2{a.z, b.z};
-    return P;
-  }
-  __device__ void next() { p += 2; }
-};
-
-// key = (f32 distance bits with the low kKeyBits cleared) | local id, as ONE
-// v_and_or_b32 (the mask held in a VGPR, the id in an SGPR: the compiler
-// otherwise emits and + or / or3). lid MUST be wave-uniform: a divergent
-// value would be read from the first lane only.
-__device__ __forceinline__ uint32_t knn_key(float d, uint32_t vmask, uint32_t lid) {
-#ifdef NAVGPU_NO_ASM_KEY
-  return (__float_as_uint(d) & vmask) | lid;
-#else
-  uint32_t k;
-  asm("v_and_or_b32 %0, %1, %2, %3" : "=v"(k) : "v"(__float_as_uint(d)), "v"(vmask), "s"(lid));
-  return k;
-#endif
-}
-
-template <int K, int NR, class Runs, class CurF, class GposF>
-__device__ __forceinline__ void knn_one(
-    const GridParams &G, const TRec *__restrict__ tsort, const double qv[3],
-    const int c[3], size_t q, Runs runs, CurF cursor, GposF fgpos,
-    int32_t *__restrict__ oidx, double *__restrict__ odist, const KnnLists &L_) {
-  // NR = 9: the block as 9 runs (run | offset ids); NR = 1: one contiguous
-  // range (the column-major tile), the whole key id is the offset
-  constexpr int kOffBits = NR == 1 ? kKeyBits : kRunOffBits;
-  static_assert(NR == 1 || NR == 9, "a 3x3x3 block is 1 or 9 ranges");
-  NV_STAMP(ts0);
-  const double qr[3] = {qv[0] - G.o[0], qv[1] - G.o[1], qv[2] - G.o[2]};
-  const float qf[3] = {(float)qr[0], (float)qr[1], (float)qr[2]};
-  // |f32 difference - exact difference| <= dl: each operand rounded to f32
-  // once (<= 2^-24 |v| each), one f32 subtraction (<= 2^-24 |difference|)
-  const double Dq = fmax(G.emax + G.h,
-                         fmax(fabs(qr[0]), fmax(fabs(qr[1]), fabs(qr[2]))));
-  const double dl = Dq * 0x1p-22;
-  constexpr int KL = K + 1;
-  uint32_t key[KL];
-#pragma unroll
-  for (int s = 0; s < KL; ++s) key[s] = kNoKey;
-  bool overflow = false;  // a run longer than the key's offset field
-  const f2 qx2 = {qf[0], qf[0]}, qy2 = {qf[1], qf[1]}, qz2 = {qf[2], qf[2]};
-  auto dist2 = [&](const Pair3 &a) {  // packed f32 squared distances
-    const f2 fx2 = a.x - qx2, fy2 = a.y - qy2, fz2 = a.z - qz2;
-    return __builtin_elementwise_fma(fz2, fz2, __builtin_elementwise_fma(fy2, fy2, fx2 * fx2));
-  };
-  auto ins = [&](uint32_t kk) {  // keep the K+1 smallest keys sorted
-#ifndef NAVGPU_DBG_NOINSERT
-#pragma unroll
-    for (int s = K; s > 0; --s) key[s] = umed3(key[s - 1], key[s], kk);
-#endif
-    key[0] = min(key[0], kk);
-  };
-  constexpr uint32_t kOffMask = (1u << kOffBits) - 1;
-  const uint32_t vmask = ~kKeyMask;
-#pragma unroll 1
-  for (int r = 0; r < NR; ++r) {
-    int t0, t1;
-    runs(r, t0, t1);
-    const int ta = t0 & ~1;
-    const int np = (t1 - ta + 1) >> 1;  // pairs the run touches
-    overflow |= (t1 - ta) > (1 << kOffBits);
-    const uint32_t rid = (uint32_t)r << kOffBits;
-    auto cur = cursor(ta);
-    if (np > 0) {  // first pair: may start before the run (odd t0) or end past it
-      const f2 d = dist2(cur.load());
-      uint32_t k0 = knn_key(d[0], vmask, rid);
-      uint32_t k1 = knn_key(d[1], vmask, rid + 1);
-      if (ta < t0) k0 = kNoKey;
-      if (ta + 1 >= t1) k1 = kNoKey;
-      ins(k0);
-      ins(k1);
-      cur.next();
-    }
-    // interior pairs: both records inside the run, no masks; the key's local
-    // id is the wave-uniform pair counter
-    // exit on the per-lane cursor reaching the last pair (one compare on the
-    // address the loop advances anyway, no separate per-lane trip counter).
-    // Only entered with np >= 3, so `last` lies past `cur`: LDS addresses
-    // start at 0, and a cursor before the run's start would wrap around.
-    if (np > 2) {
-      const auto last = cursor(ta + 2 * (np - 1));
-      uint32_t v2 = 2;
-#ifndef NAVGPU_KNN_UNROLL
-#define NAVGPU_KNN_UNROLL 1
-#endif
-#pragma unroll NAVGPU_KNN_UNROLL
-      do {
-        const f2 d = dist2(cur.load());
-        const uint32_t lid = rid | (v2 & kOffMask);
-        ins(knn_key(d[0], vmask, lid));
-        ins(knn_key(d[1], vmask, lid + 1));
-        cur.next();
-        v2 += 2;
-      } while (cur.p < last.p);
-    }
-    if (np > 1) {  // last pair: may end past the run
-      const f2 d = dist2(cur.load());
-      const uint32_t lid = rid | ((uint32_t)(2 * (np - 1)) & kOffMask);
-      // lid depends on the lane's np here: divergent, so the plain and + or
-      // (knn_key wants a wave-uniform id in an SGPR)
-      uint32_t k1 = (__float_as_uint(d[1]) & vmask) | (lid + 1);
-      if (ta + 2 * (np - 1) + 1 >= t1) k1 = kNoKey;
-      ins((__float_as_uint(d[0]) & vmask) | lid);
-      ins(k1);
-    }
-  }
-  NV_STAMP(ts1);
-  NV_STAMP_ADD(3, ts0, ts1);
-  // anything outside the block (x +- sx, y +- 1, z +- 1 cells) is at least L away
-  const double L = block_reach(G, qv, c, 1);
-  double B = INFINITY;  // lower bound on the exact dsq of every excluded point
-  if (L < INFINITY) {
-    const double Lg = L - 2.0 * G.delta;
-    B = Lg > 0.0 ? Lg * Lg : 0.0;
-  }
-  if (key[K] != kNoKey) {
-    const double V = (double)__uint_as_float(key[K] & ~kKeyMask);
-    const double err = V * 0x1p-20 + 4.0 * dl * __builtin_sqrt(V) + 4.0 * dl * dl;
-    B = fmin(B, V - err);
-  }
-  bool ok = !overflow && Dq < 1e17;
-  // exact f64 re-evaluation of the K best keys. All loads are issued
-  // unconditionally (an empty slot re-reads slot 0) so their latencies
-  // overlap; coordinates come from the cell-sorted copy (L2-local). The
-  // (K+1)-th key V is the smallest of every candidate left out, so B above
-  // bounds them all: a left-out candidate nearer than the K-th cannot pass
-  // the certificate, and V's own exact distance is never needed.
-  double ed[K];
-  int ei[K];
-#ifdef NAVGPU_DBG_NOEXACT
-  if (false) {
-#else
-  if (key[0] != kNoKey) {
-#endif
-    int gpos[K];
-    bool val[K];
-#pragma unroll
-    for (int s = 0; s < K; ++s) {
-      val[s] = key[s] != kNoKey;
-      const int l = (int)((val[s] ? key[s] : key[0]) & kKeyMask);
-#ifdef NAVGPU_DBG_NODECODE  // timing-only ablation: every slot decodes in run 0
-      const int r = 0, off = l & (int)kOffMask;
-#else
-      const int r = NR == 1 ? 0 : min(l >> kOffBits, NR - 1), off = l & (int)kOffMask;
-#endif
-      int t0, t1;
-      runs(r, t0, t1);
-      // record, in the fetch index space; clamped into the run so that a
-      // corrupt id can never address outside the staged/sorted arrays
-      const int p = min(max((t0 & ~1) + off, t0), max(t1 - 1, t0));
-      gpos[s] = fgpos(p);
-    }
-#pragma unroll
-    for (int s = 0; s < K; ++s) {
-#ifdef NAVGPU_DBG_NOF64  // timing-only ablation: f32 key as the distance
-      const double dsq = (double)__uint_as_float(key[s] & ~kKeyMask) + gpos[s] * 1e-30;
-      ei[s] = val[s] ? gpos[s] : -1;
-#else
-      // x, y as one 16-B load, z + idx as one 12-B load (the pad is never read)
-      const TRec *tp = tsort + gpos[s];
-      const double2 xy = *(const double2 *)&tp->x;
-      const double pz = tp->z;
-      const int pid = tp->idx;
-      const double ddx = xy.x - qv[0], ddy = xy.y - qv[1], ddz = pz - qv[2];
-      const double dsq = ddx * ddx + ddy * ddy + ddz * ddz;  // utils/kdtree.c:16
-      ei[s] = val[s] ? pid : -1;
-#endif
-      ed[s] = ei[s] >= 0 ? __builtin_sqrt(dsq) : INFINITY;
-      // an inf/NaN distance is never a neighbour (kdtree.c:117)
-      if (ei[s] >= 0 && !(ed[s] < INFINITY)) {
-        ed[s] = INFINITY;
-        ei[s] = -1;
-        ok = false;
-      }
-    }
-
-  } else {
-#pragma unroll
-    for (int s = 0; s < K; ++s) {
-      ed[s] = INFINITY;
-      ei[s] = -1;
-    }
-  }
-  // order by (distance, index): the truncated-key order is almost always
-  // right, and a misordered survivor sits next to its place. Bubble passes
-  // run until no lane of the wave is out of order, usually one: some lane of
-  // a wave is misordered about every other batch, so a fixed K-1 passes
-  // cost a large share of the scan (NAVGPU_SORT_FIXED restores them).
-  bool sorted = true;
-#pragma unroll
-  for (int s = 1; s < K; ++s) sorted &= !knn_less(ed[s], ei[s], ed[s - 1], ei[s - 1]);
-#if defined(NAVGPU_DBG_NOSORT)  // timing-only ablation: no ordering pass
-  if (false) {
-#pragma unroll 1
-    for (int pass = 0; pass < K - 1; ++pass) {
-#elif defined(NAVGPU_SORT_FIXED)
-  if (!sorted) {
-#pragma unroll 1
-    for (int pass = 0; pass < K - 1; ++pass) {
-#else
-  {
-#pragma unroll 1
-    for (int pass = 0; pass < K - 1 && __any(!sorted); ++pass) {
-#endif
-#pragma unroll
-      for (int u = 1; u < K; ++u) {
-        const bool sw = knn_less(ed[u], ei[u], ed[u - 1], ei[u - 1]);
-        const double td = ed[u];
-        const int ti = ei[u];
-        ed[u] = sw ? ed[u - 1] : ed[u];
-        ei[u] = sw ? ei[u - 1] : ei[u];
-        ed[u - 1] = sw ? td : ed[u - 1];
-        ei[u - 1] = sw ? ti : ei[u - 1];
-      }
-#ifndef NAVGPU_SORT_FIXED
-      sorted = true;
-#pragma unroll
-      for (int s = 1; s < K; ++s) sorted &= !knn_less(ed[s], ei[s], ed[s - 1], ei[s - 1]);
-#endif
-    }
-  }
-  const double dk = ed[K - 1];
-  const double dk2 = dk * dk;  // >= the exact K-th dsq (sqrt rounds to nearest)
-  if (dk < INFINITY)
-    ok = ok && B > dk2 * (1.0 + 0x1p-46);
-  else
-    ok = ok && B == INFINITY;  // fewer than K neighbours: only if all was seen
-#if defined(NAVGPU_DBG_NOINSERT) || defined(NAVGPU_DBG_NOEXACT) || \
-    defined(NAVGPU_DBG_NOF64) || defined(NAVGPU_DBG_NOSTAGE) || \
-    defined(NAVGPU_DBG_NODECODE) || defined(NAVGPU_DBG_NOSORT) || \
-    defined(NAVGPU_DBG_STAGE_ONCE)
-  ok = true;  // timing-only ablation builds: never take the slow path
-#endif
-  if (ok) {
-#ifdef NAVGPU_DBG_NOOUT  // timing-only ablation: one store per query, data kept live
-    double acc = 0.0;
-    int iacc = 0;
-#pragma unroll
-    for (int s = 0; s < K; ++s) {
-      acc += ed[s];
-      iacc ^= ei[s];
-    }
-    oidx[q * K] = iacc + (int)acc;
-#else
-    // a query's K results are contiguous: 16-B stores when K allows and the
-    // host found both outputs 16-B aligned (L_.vec_out)
-    if constexpr (K % 4 == 0) {
-      if (L_.vec_out) {
-#pragma unroll
-        for (int s = 0; s < K; s += 4)
-          *(int4 *)(oidx + q * K + s) = make_int4(ei[s], ei[s + 1], ei[s + 2], ei[s + 3]);
-#pragma unroll
-        for (int s = 0; s < K; s += 2)
-          *(double2 *)(odist + q * K + s) = make_double2(ed[s], ed[s + 1]);
-        return;
-      }
-    }
-#pragma unroll
-    for (int s = 0; s < K; ++s) {
-      oidx[q * K + s] = ei[s];
-      odist[q * K + s] = ed[s];
-    }
-#endif
-  } else {
-    // K listed points have dsq <= dk2: a valid starting bound for the slow
-    // path, which runs in its own launch (k_knn_slow). Not after an overfull
-    // run: its keys' offsets wrapped, so two slots can decode to the same
-    // record and the list may hold fewer than K distinct points (a bound
-    // from it can exclude a true neighbour); the slow path then starts from
-    // an infinite bound (the ring search).
-    const int e = atomicAdd(L_.n_slow, 1);
-    L_.slow_q[e] = (int)q;
-    L_.slow_thr[e] = (dk < INFINITY && !overflow) ? dk2 * (1.0 + 0x1p-46) : INFINITY;
-  }
-  NV_STAMP(ts2);
-  NV_STAMP_ADD(4, ts1, ts2);
-  NV_STAMP_ADD(5, 0ull, 1ull);
-}
-
-#ifndef NAVGPU_TILE_THREADS
-#define NAVGPU_TILE_THREADS 192  // 3 waves: a ~150-query tile fills them
-#endif
-constexpr int kTileThreads = NAVGPU_TILE_THREADS;
-constexpr int kTileRec = NAVGPU_TILE_REC;  // records staged per tile (16 B each)
-#ifndef NAVGPU_STAGE_U
-#define NAVGPU_STAGE_U 2  // records per thread per staging batch (4: 188.8 us, 8: 140 VGPRs, one block fewer per CU)
-#endif
-
-// Global-mode exact k-NN over tiles of W consecutive cells of one grid row.
-// A tile stages the 9 neighbouring row segments (cells xa-1 .. xb+1) of the
-// cell-sorted target records into LDS with coalesced loads, then its threads
-// run the tile's (cell-sorted) queries against LDS. Tiles are dealt to the
-// 8 XCDs in contiguous ranges (block b runs on XCD b % 8 under the observed
-// round-robin placement; a different placement only costs L2 hits), so each
-// XCD's L2 holds only its slab of the cloud.
-// The LDS tile is COLUMN-major: for each x cell j of the segment, the records
-// of its 9 (y, z) rows follow one another. A query's 3x3x3 block (columns
-// x-1 .. x+1, all 9 rows) is then one contiguous record range, walked as one
-// loop: a wave's trip count is the longest block among its lanes (neighbouring
-// blocks share 18 of 27 cells), not the sum over 9 runs of each run's longest,
-// and there is one run setup and one masked pair per query instead of 9.
-// GLOBAL = false: the tile pass; a tile whose segments exceed the LDS budget
-// is appended to the overflow list. GLOBAL = true: the overflow tiles, read
-// straight from the global record array as 9 runs.
-template <int K, bool GLOBAL>
-#ifndef NAVGPU_KNN_MINW
-#define NAVGPU_KNN_MINW 1
-#endif
-#ifdef NAVGPU_KNN_WPE
-#define NAVGPU_KNN_ATTR __attribute__((amdgpu_waves_per_eu(NAVGPU_KNN_WPE)))
-#else
-#define NAVGPU_KNN_ATTR
-#endif
-__global__ __launch_bounds__(kTileThreads, NAVGPU_KNN_MINW) NAVGPU_KNN_ATTR void k_knn(
-    const GridParams *__restrict__ gp, const int *__restrict__ start,
-    const Rec16 *__restrict__ rec, const TRec *__restrict__ tsort,
-    const double *__restrict__ qs, const int *__restrict__ qstart,
-    const int *__restrict__ qperm, int32_t *__restrict__ oidx,
-    double *__restrict__ odist, KnnLists L_) {
-  // pair-interleaved records: pair P = LDS slots 2P, 2P+1 as x0 x1 y0 y1 z0 z1
-  // g0 g1 (32 B; g = the record's cell-sorted position), so one b128 + one
-  // b64 read gives packed operands; two spare pairs absorb the read-ahead
-  // past a range's end
-  __shared__ __attribute__((aligned(16))) float spair[GLOBAL ? 8 : 2 * kZgOff];
-  // soff[r][i] = first record of cell xa - sx + i of row r; then, in place
-  // (tile pass), cbase[r][j]: the LDS slot of the record at cell-sorted
-  // position g of cell (row r, column j) is cbase[r][j] + g
-  __shared__ int soff[9][kTileCols];
-  __shared__ int colst[GLOBAL ? 1 : kTileCols];  // first slot of column j (j = 0: cell xa - sx)
-  __shared__ int scratch[kTileThreads / kWave + 1];
-  const GridParams G = *gp;
-  const int W = G.tile_w, sx = G.sx;
-  const int tpr = (G.g[0] + W - 1) / W;
-  long long t_hi, step, first;
-  if (GLOBAL) {
-    t_hi = *L_.n_ovf;
-    first = blockIdx.x;
-    step = gridDim.x;
-  } else {
-    const long long ntiles = (long long)tpr * G.g[1] * G.g[2];
-    const int xcd = blockIdx.x & 7;
-    t_hi = ntiles * (xcd + 1) / 8;
-    first = ntiles * xcd / 8 + (blockIdx.x >> 3);
-    step = gridDim.x >> 3;
-  }
-  for (long long it = first; it < t_hi; it += step) {
-    NV_STAMP(tb0);
-    const long long tile = GLOBAL ? (long long)L_.ovf_tiles[it] : it;
-    const int row = (int)(tile / tpr), chunk = (int)(tile % tpr);
-    const int y = row % G.g[1], z = row / G.g[1];
-    const int xa = chunk * W, xb = min(xa + W, G.g[0]) - 1;
-    const int ncell = xb - xa + 2 + 2 * sx;  // soff entries per row: cells xa-sx .. xb+sx+1
-#ifdef NAVGPU_DBG_STAGE_ONCE  // timing-only ablation: the first tile's staging serves all
-    if (it == first) {
-#endif
-    // staging is latency-bound: every thread issues all its global loads
-    // before it writes any of them to LDS
-    // soff: the 9 rows (uniform loop, no index division), all loads first
-    for (int i0 = 0; i0 < ncell; i0 += (int)blockDim.x) {
-      const int i = i0 + (int)threadIdx.x;
-      int v[9];
-#pragma unroll
-      for (int r = 0; r < 9; ++r) {
-        int dy, dz;
-        run_dydz(r, dy, dz);
-        const int yy = y + dy, zz = z + dz;
-        v[r] = 0;
-        if (i < ncell && yy >= 0 && yy < G.g[1] && zz >= 0 && zz < G.g[2]) {
-          const int x = min(max(xa - sx + i, 0), G.g[0]);  // x = gx: row end
-          v[r] = start[(zz * G.g[1] + yy) * G.g[0] + x];
-        }
-      }
-      if (i < ncell) {
-#pragma unroll
-        for (int r = 0; r < 9; ++r) soff[r][i] = v[r];
-      }
-    }
-    __syncthreads();
-    int sb[10], s0[9];  // row segment bases (staging index) and global offsets
-    if (!GLOBAL) {
-      // the copy's source order: the 9 row segments one after another
-      sb[0] = 0;
-#pragma unroll
-      for (int u = 0; u < 9; ++u) {
-        const int lo = soff[u][0];
-        sb[u + 1] = sb[u] + (soff[u][ncell - 1] - lo);
-        s0[u] = lo - sb[u];  // global = e + s0[r]
-      }
-      // the column-major layout: thread j owns column j of the W + 2 sx
-      const int ncol = ncell - 1, j = (int)threadIdx.x;
-      int n[9], sv[9], cs = 0;
-#pragma unroll
-      for (int r = 0; r < 9; ++r) {
-        sv[r] = j < ncol ? soff[r][j] : 0;
-        n[r] = j < ncol ? soff[r][j + 1] - sv[r] : 0;
-        cs += n[r];
-      }
-      int total;
-      const int cex = block_excl_scan(cs, scratch, &total);  // barriers: soff reads done
-      if (total > kTileRec) {  // uniform: defer the tile to the global pass
-        if (threadIdx.x == 0) L_.ovf_tiles[atomicAdd(L_.n_ovf, 1)] = (int)tile;
-        __syncthreads();
-        continue;
-      }
-      if (j <= ncol) colst[j] = cex;  // colst[ncol] = the total
-      if (j < ncol) {
-        int a = cex;
-#pragma unroll
-        for (int r = 0; r < 9; ++r) {
-          soff[r][j] = a - sv[r];  // cbase
-          a += n[r];
-        }
-      }
-      __syncthreads();
-      const int jmax = ncol - 1;
-      // each wave copies whole row segments (r = wave, wave + nwaves, ...):
-      // r is wave-uniform, so a record's global position is e + s0[r] with
-      // no per-record segment decode (that decode was most of the staging
-      // VALU); a batch's loads are all issued before any LDS write
-      const int lane = (int)threadIdx.x & (kWave - 1);
-      const int nwv = (int)blockDim.x / kWave;
-      constexpr int U = NAVGPU_STAGE_U;  // records per lane per batch
-      for (int r = (int)threadIdx.x / kWave; r < 9; r += nwv) {
-        const int g0 = sb[r] + s0[r], nr = sb[r + 1] - sb[r];
-        const int *cb = &soff[r][0];
-        for (int k0 = 0; k0 < nr; k0 += U * kWave) {
-          Rec16 v[U];
-#pragma unroll
-          for (int u = 0; u < U; ++u) {
-            const int k = k0 + u * kWave + lane;
-            if (k < nr) {
-#ifdef NAVGPU_DBG_NOSTAGE  // timing-only ablation: no record loads
-              v[u].x = v[u].y = v[u].z = (float)k;
-              v[u].cx = xa;
-#else
-              v[u] = rec[g0 + k];
-#endif
-            }
-          }
-#pragma unroll
-          for (int u = 0; u < U; ++u) {
-            const int k = k0 + u * kWave + lane;
-            if (k < nr) {
-              // the record's column (its cell lies in xa-sx .. xb+sx; clamped
-              // so that a corrupt value cannot address outside the tile)
-              const int g = g0 + k;
-              const int jj = min(max(v[u].cx - xa + sx, 0), jmax);
-              const int slot = cb[jj] + g;
-              float *d = spair + (slot >> 1) * 4 + (slot & 1);
-              d[0] = v[u].x;
-              d[2] = v[u].y;
-              d[kZgOff] = v[u].z;
-              d[kZgOff + 2] = __int_as_float(g);
-            }
-          }
-        }
-      }
-      __syncthreads();
-    }
-#ifdef NAVGPU_DBG_STAGE_ONCE
-    }
-#endif
-    NV_STAMP(tb1);
-    NV_STAMP_ADD(1, tb0, tb1);
-    NV_STAMP_ADD(6, 0ull, 1ull);
-    const int cell0 = (z * G.g[1] + y) * G.g[0];
-    const int q0 = qstart[cell0 + xa], q1 = qstart[cell0 + xb + 1];
-#ifdef NAVGPU_DBG_NOQUERY  // timing-only ablation: staging and barriers only
-    if (q1 < 0)
-#endif
-    for (int qi = q0 + threadIdx.x; qi < q1; qi += blockDim.x) {
-      const size_t q = (size_t)qperm[qi];
-      const double qv[3] = {qs[3 * q], qs[3 * q + 1], qs[3 * q + 2]};
-      const int c[3] = {cell_axis(qv[0], G, 0), y, z};
-      const int i = c[0] - xa;  // columns i .. i + 2 sx = cells c - sx .. c + sx
-      if (!GLOBAL) {
-        knn_one<K, 1>(G, tsort, qv, c, q,
-                      [&](int, int &t0, int &t1) {
-                        t0 = colst[i];
-                        t1 = colst[i + 2 * sx + 1];
-                      },
-                      [&](int t) { return LdsPairCursor{spair + (t >> 1) * 4}; },
-                      [&](int p) { return __float_as_int(spair[kZgOff + (p >> 1) * 4 + 2 + (p & 1)]); },
-                      oidx, odist, L_);
-      } else {
-        knn_one<K, 9>(G, tsort, qv, c, q,
-                      [&](int r, int &t0, int &t1) {
-                        t0 = soff[r][i];
-                        t1 = soff[r][i + 2 * sx + 1];
-                      },
-                      [&](int t) { return RecPairCursor{rec + t}; },
-                      [&](int p) { return p; }, oidx, odist, L_);
-      }
-    }
-    NV_STAMP(tb2);
-    NV_STAMP_ADD(2, tb1, tb2);
-    __syncthreads();
-    NV_STAMP(tb3);
-    NV_STAMP_ADD(7, tb2, tb3);
-  }
-}
-
-// insert (d, id) into the sorted exact list kd/ki if it ranks among the K
-template <int K>
-__device__ __forceinline__ void knn_insert(double *kd, int *ki, double d, int id) {
-  if (!knn_less(d, id, kd[K - 1], ki[K - 1])) return;
-  bool placed = false;
-#pragma unroll
-  for (int s = K - 1; s >= 0; --s) {
-    if (!placed) {
-      if (s > 0 && knn_less(d, id, kd[s - 1], ki[s - 1])) {
-        kd[s] = kd[s - 1];
-        ki[s] = ki[s - 1];
-      } else {
-        kd[s] = d;
-        ki[s] = id;
-        placed = true;
-      }
-    }
-  }
-}
-
-// merge the 64 lane lists kd/ki (each sorted) into md/mi: K rounds of a
-// wave (distance, index) argmin on the list heads
-template <int K>
-__device__ __forceinline__ void knn_wave_merge(double *kd, int *ki, double *md, int *mi,
-                                               int lane) {
-#pragma unroll
-  for (int s = 0; s < K; ++s) {
-    double bd = kd[0];
-    int bi = ki[0], bl = lane;
-#pragma unroll
-    for (int o = kWave / 2; o > 0; o >>= 1) {
-      const double od = __shfl_xor(bd, o, kWave);
-      const int oi = __shfl_xor(bi, o, kWave), ol = __shfl_xor(bl, o, kWave);
-      const bool take = knn_less(od, oi, bd, bi) ||
-                        (!knn_less(bd, bi, od, oi) && ol < bl);
-      bd = take ? od : bd;
-      bi = take ? oi : bi;
-      bl = take ? ol : bl;
-    }
-    md[s] = bd;
-    mi[s] = bi;
-    if (lane == bl) {  // pop the winner's head
-#pragma unroll
-      for (int u = 0; u < K - 1; ++u) {
-        kd[u] = kd[u + 1];
-        ki[u] = ki[u + 1];
-      }
-      kd[K - 1] = INFINITY;
-      ki[K - 1] = -1;
-    }
-  }
-}
-
-// f32 screen + exact f64 distance of record t against the query; inserts
-// into the lane's sorted list when within thr
-template <int K>
-__device__ __forceinline__ void knn_visit(const Rec16 &rr, size_t t,
-                                          const TRec *__restrict__ tsort,
-                                          const double qv[3], const float qf[3],
-                                          double thr, float thr_f, double *kd, int *ki) {
-  const float fx = rr.x - qf[0], fy = rr.y - qf[1], fz = rr.z - qf[2];
-  const float d2f = __builtin_fmaf(fz, fz, __builtin_fmaf(fy, fy, fx * fx));
-  if (!(d2f <= thr_f)) return;
-  const TRec tp = tsort[t];
-  const double ddx = tp.x - qv[0], ddy = tp.y - qv[1], ddz = tp.z - qv[2];
-  const double dsq = ddx * ddx + ddy * ddy + ddz * ddz;  // utils/kdtree.c:16
-  if (!(dsq <= thr)) return;
-  knn_insert<K>(kd, ki, __builtin_sqrt(dsq), tp.idx);
-}
-
-constexpr int kSlowMaxR = 3;  // one-shot cube: at most (2R+1)^2 = 49 rows
-
-// The queries k_knn could not certify, one WAVE per query, from the recorded
-// starting bound thr (K real points lie within it, so every neighbour does).
-// One-shot cube: the smallest cube of cells around the query whose outside is
-// provably beyond thr; its (y, z) rows are contiguous record ranges, counted
-// and prefix-summed across the wave so the records are dealt evenly over the
-// 64 lanes. Each lane keeps a sorted list (f32 screen, then the reference f64
-// distance); one wave merge gives the answer. An infinite bound, or a cube
-// beyond kSlowMaxR, takes the ring search: rings of cells split over the
-// lanes, merged after every ring, the merged K-th bounding the next ring.
-template <int K>
-__global__ __launch_bounds__(256) void k_knn_slow(
-    const GridParams *__restrict__ gp, const int *__restrict__ start,
-    const Rec16 *__restrict__ rec, const TRec *__restrict__ tsort,
-    const double *__restrict__ qs, int32_t *__restrict__ oidx,
-    double *__restrict__ odist, KnnLists L_) {
-  __shared__ double sd[4][kWave];  // per-wave survivor buffers (256 threads)
-  __shared__ int si[4][kWave];
-  const GridParams G = *gp;
-  const int n = *L_.n_slow;
-  const int lane = threadIdx.x & (kWave - 1);
-  const int wave = (int)((blockIdx.x * blockDim.x + threadIdx.x) / kWave);
-  const int nwaves = (int)(gridDim.x * blockDim.x / kWave);
-  const int gmax = max((G.g[0] + G.sx - 1) / G.sx, max(G.g[1], G.g[2]));
-  for (int e = wave; e < n; e += nwaves) {
-    const size_t q = (size_t)L_.slow_q[e];
-    double thr = L_.slow_thr[e];
-    const double qv[3] = {qs[3 * q], qs[3 * q + 1], qs[3 * q + 2]};
-    const double qr[3] = {qv[0] - G.o[0], qv[1] - G.o[1], qv[2] - G.o[2]};
-    const float qf[3] = {(float)qr[0], (float)qr[1], (float)qr[2]};
-    const double Dq = fmax(G.emax + G.h,
-                           fmax(fabs(qr[0]), fmax(fabs(qr[1]), fabs(qr[2]))));
-    const double dl = Dq * 0x1p-22;
-    float thr_f = f32_bound(thr, dl);
-    const int c[3] = {cell_axis(qv[0], G, 0), cell_axis(qv[1], G, 1),
-                      cell_axis(qv[2], G, 2)};
-    double kd[K], md[K];
-    int ki[K], mi[K];
-#pragma unroll
-    for (int s = 0; s < K; ++s) {
-      kd[s] = INFINITY;
-      ki[s] = -1;
-    }
-    // cube radius: everything outside cube R is at least L_R away
-    int R = -1;
-    if (thr < INFINITY) {
-      for (int r = 1; r <= kSlowMaxR; ++r) {
-        const double L = block_reach(G, qv, c, r);
-        const double Lg = L - 2.0 * G.delta;
-        if (L == INFINITY || (Lg > 0.0 && thr < Lg * Lg)) {
-          R = r;
-          break;
-        }
-      }
-    }
-    if (R > 0) {
-      const int xl = max(c[0] - R * G.sx, 0), xh = min(c[0] + R * G.sx, G.g[0] - 1);
-      const int yl = max(c[1] - R, 0), yh = min(c[1] + R, G.g[1] - 1);
-      const int zl = max(c[2] - R, 0), zh = min(c[2] + R, G.g[2] - 1);
-      const int ny = yh - yl + 1, nrows = ny * (zh - zl + 1);  // <= 49
-      int cnt = 0, b = 0;
-      if (lane < nrows) {
-        const int y = yl + lane % ny, z = zl + lane / ny;
-        if (!(box_d2(G, qv, xl, xh, y, y, z, z) > thr)) {
-          const int row = (z * G.g[1] + y) * G.g[0];
-          b = start[row + xl];
-          cnt = start[row + xh + 1] - b;
-        }
-      }
-      int pre = cnt;  // inclusive wave scan of the row counts
-#pragma unroll
-      for (int o = 1; o < kWave; o <<= 1) {
-        const int t = __shfl_up(pre, o, kWave);
-        if (lane >= o) pre += t;
-      }
-      const int total = __shfl(pre, kWave - 1, kWave);
-      pre -= cnt;  // exclusive
-      for (int j0 = 0; j0 < total; j0 += kWave) {
-        const int j = j0 + lane;
-        // row of flattened record j: the last row whose prefix is <= j
-        int lo = 0;
-#pragma unroll
-        for (int step = 32; step > 0; step >>= 1) {
-          const int cand = lo + step;
-          const int pc = __shfl(pre, cand < nrows ? cand : 0, kWave);
-          if (cand < nrows && pc <= j) lo = cand;
-        }
-        const int pb = __shfl(b, lo, kWave), pp = __shfl(pre, lo, kWave);
-        if (j < total) {
-          const size_t t = (size_t)(pb + (j - pp));
-          knn_visit<K>(rec[t], t, tsort, qv, qf, thr, thr_f, kd, ki);
-        }
-      }
-      // the lanes' survivors (usually ~K in all): compact them into LDS and
-      // rank each by counting smaller ones; more than 64 take the merge
-      int nsv = 0;
-#pragma unroll
-      for (int u = 0; u < K; ++u) nsv += kd[u] < INFINITY ? 1 : 0;
-      int off = nsv;
-#pragma unroll
-      for (int o = 1; o < kWave; o <<= 1) {
-        const int t = __shfl_up(off, o, kWave);
-        if (lane >= o) off += t;
-      }
-      const int tot = __shfl(off, kWave - 1, kWave);
-      off -= nsv;
-      if (tot <= kWave) {
-        double *bd = sd[threadIdx.x / kWave];
-        int *bi = si[threadIdx.x / kWave];
-#pragma unroll
-        for (int u = 0; u < K; ++u)
-          if (u < nsv) {
-            bd[off + u] = kd[u];
-            bi[off + u] = ki[u];
-          }
-        wave_sync_mem();
-        if (lane < tot) {
-          const double d = bd[lane];
-          const int id = bi[lane];
-          int rank = 0;
-          for (int t = 0; t < tot; ++t) rank += knn_less(bd[t], bi[t], d, id) ? 1 : 0;
-          if (rank < K) {
-            oidx[q * K + rank] = id;
-            odist[q * K + rank] = d;
-          }
-        } else if (lane < K) {  // fewer than K survivors: empty slots
-          oidx[q * K + lane] = -1;
-          odist[q * K + lane] = INFINITY;
-        }
-        wave_sync_mem();  // the buffer is reused by this wave's next query
-        continue;
-      }
-      knn_wave_merge<K>(kd, ki, md, mi, lane);
-    }
-    for (int r = 0; R < 0 && r <= gmax; ++r) {
-      // the ring's cube clipped to the grid (a degenerate axis stays 1 thick);
-      // x reaches r * sx cells
-      const int xl = max(c[0] - r * G.sx, 0), xh = min(c[0] + r * G.sx, G.g[0] - 1);
-      const int yl = max(c[1] - r, 0), yh = min(c[1] + r, G.g[1] - 1);
-      const int zl = max(c[2] - r, 0), zh = min(c[2] + r, G.g[2] - 1);
-      const int bx = xh - xl + 1, by = yh - yl + 1, bz = zh - zl + 1;
-      const int nbox = bx * by * bz;
-      for (int u = lane; u < nbox; u += kWave) {
-        const int x = xl + u % bx, y = yl + (u / bx) % by, z = zl + u / (bx * by);
-        if (max((abs(x - c[0]) + G.sx - 1) / G.sx, max(abs(y - c[1]), abs(z - c[2]))) != r)
-          continue;
-        if (box_d2(G, qv, x, x, y, y, z, z) > thr) continue;
-        const int cell = (z * G.g[1] + y) * G.g[0] + x;
-        const int b = start[cell], en = start[cell + 1];
-        for (int t = b; t < en; ++t)
-          knn_visit<K>(rec[t], (size_t)t, tsort, qv, qf, thr, thr_f, kd, ki);
-      }
-      knn_wave_merge<K>(kd, ki, md, mi, lane);
-      // lane 0 carries the merged list into the next ring
-#pragma unroll
-      for (int s = 0; s < K; ++s) {
-        kd[s] = lane == 0 ? md[s] : INFINITY;
-        ki[s] = lane == 0 ? mi[s] : -1;
-      }
-      if (md[K - 1] < INFINITY) {
-        thr = fmin(thr, md[K - 1] * md[K - 1] * (1.0 + 0x1p-46));
-        thr_f = f32_bound(thr, dl);
-      }
-      const double L = block_reach(G, qv, c, r);
-      if (L == INFINITY) break;
-      const double Lg = L - 2.0 * G.delta;
-      if (Lg > 0.0 && thr < Lg * Lg) break;  // all points with dsq <= thr seen
-    }
-    if (lane == 0) {
-#pragma unroll
-      for (int s = 0; s < K; ++s) {
-        oidx[q * K + s] = mi[s];
-        odist[q * K + s] = md[s];
-      }
-    }
-  }
-}
-
 }  // namespace
 
 // =================================================================== host
-struct navgpu_ctx {
-  int device = 0;
-  hipStream_t stream = nullptr;
-  bool own_stream = false;
-  std::map<int, std::pair<void *, size_t>> bufs;  // grow-only workspace
-  bool timing = false;
-  std::map<std::string, std::vector<std::pair<hipEvent_t, hipEvent_t>>> ev;
-  std::vector<hipEvent_t> free_ev;
-  std::vector<double> tan_c, tan_r;
-  int tan_R = -1, tan_C = -1;
-  hipStream_t aux = nullptr;                 // side stream (pair path: curvature)
-  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
-  double knn_occ = 5.0;  // target points per h^3 grid cell (NAVGPU_KNN_OCC)
-  int knn_sx = NAVGPU_KNN_SX;  // x cells per h (NAVGPU_KNN_SX)
-  int knn_blocks = 0;    // k_knn blocks per XCD, 0 = auto (NAVGPU_KNN_BLOCKS)
-  bool knn_stats = false;
-  int screen_rows = 0, screen_S = 0;  // last screened rows_match call (tie diagnostic)
-};
-
-namespace {
-
-enum Slot {
-  kBBox = 1, kParams, kCnt, kStart, kBSum, kCellId, kSlotBuf, kRec, kTan,
-  kKdFc, kKdP, kKdT, kQStart, kQCell, kQSlot, kQPerm, kStats, kOvf, kSlowQ,
-  kSlowThr, kTSort, kRowMaskS, kRowMaskT, kRowTie, kCorrEnt, kCorrN, kCorrSums, kKdPtmp, kKdSel,
-  kH0 = 100, kH1, kH2, kH3, kH4, kH5,
-};
+namespace nv {
 
 int ws_get(navgpu_ctx *ctx, int slot, size_t bytes, void **out) {
   auto &b = ctx->bufs[slot];
@@ -3522,48 +2037,28 @@ int ws_get(navgpu_ctx *ctx, int slot, size_t bytes, void **out) {
   return NAVGPU_OK;
 }
 
-template <class T>
-int ws(navgpu_ctx *ctx, int slot, size_t count, T **out) {
-  void *p;
-  int rc = ws_get(ctx, slot, count * sizeof(T), &p);
-  *out = (T *)p;
-  return rc;
+int ensure_aux(navgpu_ctx *ctx) {
+  if (!ctx->aux) {
+    HIP_TRY(hipStreamCreateWithFlags(&ctx->aux, hipStreamNonBlocking));
+    HIP_TRY(hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming));
+    HIP_TRY(hipEventCreateWithFlags(&ctx->ev_join, hipEventDisableTiming));
+  }
+  return NAVGPU_OK;
 }
 
-#define RC(x)                    \
-  do {                           \
-    int rc_ = (x);               \
-    if (rc_ != NAVGPU_OK) return rc_; \
-  } while (0)
+int launch_curvature(const double *pts0, int32_t *mask0, double *curv0,
+                     const double *pts1, int32_t *mask1, double *curv1, int R, int C,
+                     hipStream_t stream) {
+  CurvJob J = {{pts0, pts1}, {mask0, mask1}, {curv0, curv1}};
+  dim3 grid((C + kCurvTile - 1) / kCurvTile, R, pts1 ? 2 : 1);
+  hipLaunchKernelGGL(k_curvature, grid, dim3(kCurvTile), 0, stream, J, R, C);
+  CHECK_LAUNCH("k_curvature");
+  return NAVGPU_OK;
+}
 
-struct TimedRegion {
-  navgpu_ctx *ctx;
-  const char *name;
-  hipEvent_t a = nullptr, b = nullptr;
-  hipEvent_t take() {
-    if (!ctx->free_ev.empty()) {
-      hipEvent_t e = ctx->free_ev.back();
-      ctx->free_ev.pop_back();
-      return e;
-    }
-    hipEvent_t e = nullptr;
-    if (hipEventCreate(&e) != hipSuccess) return nullptr;
-    return e;
-  }
-  hipStream_t st;
-  TimedRegion(navgpu_ctx *c, const char *n, hipStream_t on = nullptr)
-      : ctx(c), name(n), st(on ? on : c->stream) {
-    if (!ctx->timing) return;
-    a = take();
-    b = take();
-    if (a && b) (void)hipEventRecord(a, st);
-  }
-  ~TimedRegion() {
-    if (!ctx->timing || !a || !b) return;
-    (void)hipEventRecord(b, st);
-    ctx->ev[name].push_back({a, b});
-  }
-};
+}  // namespace nv
+
+namespace {
 
 // dynamic LDS a tree-building kernel may request: the device limit minus
 // the static LDS of block_nth_element (pointer-jumping words + counts)
@@ -3601,10 +2096,6 @@ int set_lds(Kern k, int bytes) {
   return NAVGPU_OK;
 }
 
-unsigned grid1d(size_t n, int block) {
-  return (unsigned)((n + block - 1) / block);
-}
-
 }  // namespace
 
 // ------------------------------------------------------------------ C ABI
@@ -3636,11 +2127,15 @@ int navgpu_create(int device, void *stream, navgpu_ctx **out) {
   if (const char *o = getenv("NAVGPU_KNN_BLOCKS")) c->knn_blocks = atoi(o);
   if (const char *o = getenv("NAVGPU_KNN_SX")) {
     const int v = atoi(o);
-    if (v >= 1 && v <= kMaxSx) c->knn_sx = v;
+    if (v >= 1 && v <= kKnnMaxSx) c->knn_sx = v;
   }
   if (const char *o = getenv("NAVGPU_KNN_OCC")) {
     const double v = atof(o);
     if (v > 0.05 && v < 1000) c->knn_occ = v;
+  }
+  if (const char *o = getenv("NAVGPU_KNN_LAMBDA")) {
+    const double v = atof(o);
+    if (v >= 1.0 && v < 1e6) c->knn_lambda = v;
   }
   if (stream) {
     c->stream = (hipStream_t)stream;
@@ -3699,14 +2194,6 @@ int navgpu_sync(navgpu_ctx *ctx) {
   return NAVGPU_OK;
 }
 
-static int ensure_aux(navgpu_ctx *ctx) {
-  if (!ctx->aux) {
-    HIP_TRY(hipStreamCreateWithFlags(&ctx->aux, hipStreamNonBlocking));
-    HIP_TRY(hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming));
-    HIP_TRY(hipEventCreateWithFlags(&ctx->ev_join, hipEventDisableTiming));
-  }
-  return NAVGPU_OK;
-}
 
 int navgpu_side_mark(navgpu_ctx *ctx) {
   ARG_CHECK(ctx);
@@ -3768,33 +2255,15 @@ int navgpu_debug_stamps(unsigned long long *out16) {
 #ifdef NAVGPU_STAMPS
   HIP_TRY(hipDeviceSynchronize());
   HIP_TRY(hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_stamps), 16 * 8));
-  unsigned long long z[16] = {0};
+  unsigned long long z[16] = {0}, k[16];
   HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), z, 16 * 8));
+  RC(knn_stamps_take(k));
+  for (int i = 0; i < 16; ++i) out16[i] += k[i];
   return NAVGPU_OK;
 #else
   (void)out16;
   return NAVGPU_EINVAL;
 #endif
-}
-
-long long navgpu_knn_fallbacks(navgpu_ctx *ctx) {
-  if (!ctx) return -1;
-  auto it = ctx->bufs.find(kStats);
-  if (it == ctx->bufs.end() || !it->second.first) return -1;
-  int v[2] = {0, 0};
-  if (hipStreamSynchronize(ctx->stream) != hipSuccess) return -1;
-  if (hipMemcpy(v, it->second.first, 8, hipMemcpyDeviceToHost) != hipSuccess) return -1;
-  return (long long)v[1];
-}
-
-long long navgpu_knn_overflows(navgpu_ctx *ctx) {
-  if (!ctx) return -1;
-  auto it = ctx->bufs.find(kStats);
-  if (it == ctx->bufs.end() || !it->second.first) return -1;
-  int v[2] = {0, 0};
-  if (hipStreamSynchronize(ctx->stream) != hipSuccess) return -1;
-  if (hipMemcpy(v, it->second.first, 8, hipMemcpyDeviceToHost) != hipSuccess) return -1;
-  return (long long)v[0];
 }
 
 long long navgpu_rows_tie_rows(navgpu_ctx *ctx) {
@@ -4398,231 +2867,6 @@ int navgpu_download(navgpu_ctx *ctx, void *dst, const void *src, size_t bytes) {
   ARG_CHECK(dst && src);
   HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, ctx->stream));
   return NAVGPU_OK;
-}
-
-// ------------------------------------------------------------ global k-NN
-}  // extern "C"
-
-// The k-NN call (navgpu_knn_dev).
-static int knn_run(navgpu_ctx *ctx, const double *tgt, size_t nt, const double *queries,
-                   size_t nq, int k, int32_t *idx, double *dist) {
-  ARG_CHECK(ctx && k >= 1 && k <= 16);
-  ARG_CHECK(nt < (size_t)INT32_MAX / 2 && nq < (size_t)INT32_MAX);
-  if (!nq) return NAVGPU_OK;
-  ARG_CHECK(queries && idx && dist && (tgt || nt == 0));
-  const double occ = ctx->knn_occ;
-  const int sx = ctx->knn_sx;
-  const long long capl = (long long)((double)nt / occ) * 2 * sx + 1024;
-  ARG_CHECK(capl < INT32_MAX / 2);
-  const int cap = (int)capl;
-  const int nscan = cap + 1;  // start[] has one entry past the last cell
-  // binning geometry (k_bin_*): coarse buckets of 2^shift cells, at most
-  // kBinMaxBuckets of them; chunks of P points per histogram block
-  // at least one cell per fine-pass thread (the fine scan gives each thread a
-  // contiguous run of 2^shift / threads cells)
-  int shift = NAVGPU_BIN_MIN_SHIFT;
-  while ((1 << shift) < kBinFineThreads) ++shift;
-  while (((long long)nscan + (1 << shift) - 1) >> shift > kBinMaxBuckets) ++shift;
-  if (shift > kBinMaxShift) {
-    set_err("knn: %zu targets exceed the binning capacity", nt);
-    return NAVGPU_ERANGE;
-  }
-  BinJob J;
-  J.shift = shift;
-  J.nb = (int)(((long long)nscan + (1 << shift) - 1) >> shift);
-  const size_t ns[2] = {nt, nq};
-  long long ntab = 0;
-  for (int side = 0; side < 2; ++side) {
-    BinSide &S = J.s[side];
-    S.n = (int)ns[side];
-    S.P = (int)std::max<size_t>(NAVGPU_BIN_P, (ns[side] / 2000 + 256) / 256 * 256);
-    S.nblk = (int)std::max<size_t>(1, (ns[side] + S.P - 1) / S.P);
-    S.tab = (int)ntab;
-    S.sub = side ? (int)nt : 0;
-    ntab += (long long)J.nb * S.nblk + 1;
-  }
-  const int nbs = (int)((ntab + kScanTile - 1) / kScanTile);
-  if (nbs > kScanTile) {
-    set_err("knn: binning table of %lld entries exceeds the scan capacity", ntab);
-    return NAVGPU_ERANGE;
-  }
-  const int nparts = (int)std::min<size_t>(kBBoxBlocks, std::max<size_t>(1, grid1d(nt, 256)));
-  double *part;
-  GridParams *gp;
-  int *tab, *offs, *tstart, *qstart, *bsum, *qperm;
-  Rec16 *rec = nullptr;
-  TRec *tsort = nullptr;
-  BinPt *bin_t = nullptr;
-  int2 *bin_q;
-  RC(ws(ctx, kBBox, (size_t)kBBoxBlocks * 6, &part));
-  RC(ws(ctx, kParams, 1, &gp));
-  RC(ws(ctx, kCnt, (size_t)ntab, &tab));
-  RC(ws(ctx, kCellId, (size_t)ntab, &offs));
-  RC(ws(ctx, kStart, nscan, &tstart));
-  RC(ws(ctx, kQStart, nscan, &qstart));
-  RC(ws(ctx, kBSum, nbs, &bsum));
-  int *counters;
-  RC(ws(ctx, kStats, 4, &counters));  // [n_ovf, n_slow, pad, pad], zeroed by k_grid_params
-  if (nt) {
-    RC(ws(ctx, kSlotBuf, nt, &bin_t));
-    RC(ws(ctx, kRec, nt + 2, &rec));  // + 2: a last pair may read one past the end
-    RC(ws(ctx, kTSort, nt, &tsort));
-  }
-  RC(ws(ctx, kQCell, nq, &bin_q));
-  RC(ws(ctx, kQPerm, nq, &qperm));
-  J.s[0].p = tgt;
-  J.s[1].p = queries;
-  J.s[0].start = tstart;
-  J.s[1].start = qstart;
-  J.bin_t = bin_t;
-  J.bin_q = bin_q;
-  J.rec = rec;
-  J.tsort = tsort;
-  J.qperm = qperm;
-  hipStream_t s = ctx->stream;
-  {
-    TimedRegion tb(ctx, "knn_build");
-    if (nt) {
-      hipLaunchKernelGGL(k_bbox_partial, dim3(nparts), dim3(256), 0, s, tgt, nt, part);
-      CHECK_LAUNCH("k_bbox_partial");
-    }
-    hipLaunchKernelGGL(k_grid_params, dim3(1), dim3(256), 0, s, part, nt ? nparts : 0, nt,
-                       cap, occ, sx, nq, gp, counters);
-    CHECK_LAUNCH("k_grid_params");
-    const dim3 gb(J.s[0].nblk + J.s[1].nblk);
-    hipLaunchKernelGGL(k_bin_hist, gb, dim3(256), 0, s, J, gp, tab);
-    CHECK_LAUNCH("k_bin_hist");
-    const int ntabi = (int)ntab;
-    hipLaunchKernelGGL(k_scan_sums, dim3(nbs), dim3(kScanBlock), 0, s, tab, ntabi, bsum);
-    CHECK_LAUNCH("k_scan_sums");
-    hipLaunchKernelGGL(k_scan_apply, dim3(nbs), dim3(kScanBlock), 0, s, tab, ntabi, bsum,
-                       offs);
-    CHECK_LAUNCH("k_scan_apply");
-    hipLaunchKernelGGL(k_bin_scatter, gb, dim3(256), 0, s, J, gp, (const int *)offs);
-    CHECK_LAUNCH("k_bin_scatter");
-    const size_t lds = (size_t)4 << shift;
-    if (lds > 48 * 1024)
-      HIP_TRY(hipFuncSetAttribute((const void *)k_bin_fine,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    hipLaunchKernelGGL(k_bin_fine, dim3(2 * J.nb), dim3(kBinFineThreads), lds, s, J, gp,
-                       (const int *)offs, nscan);
-    CHECK_LAUNCH("k_bin_fine");
-  }
-  KnnLists lists;
-  RC(ws(ctx, kOvf, (size_t)cap + 1, &lists.ovf_tiles));
-  RC(ws(ctx, kSlowQ, nq, &lists.slow_q));
-  RC(ws(ctx, kSlowThr, nq, &lists.slow_thr));
-  lists.n_ovf = counters;
-  lists.n_slow = counters + 1;
-  lists.vec_out = ((uintptr_t)idx % 16 == 0 && (uintptr_t)dist % 16 == 0) ? 1 : 0;
-#ifdef NAVGPU_SCALAR_OUT
-  lists.vec_out = 0;
-#endif
-  TimedRegion tr(ctx, "knn_query");
-  // tiles are walked by a grid of 8 x nbx blocks (block b -> XCD b % 8, the
-  // placement HW_REG_XCC_ID reports); more blocks than resident slots
-  // balance the uneven tiles (measured plateau from ~512 per XCD at 1M)
-  const int nbx = ctx->knn_blocks > 0
-                      ? ctx->knn_blocks
-                      : (int)std::min<size_t>(768, std::max<size_t>(1, nq / 1300 + 1));
-  const dim3 g(8 * nbx), b(kTileThreads);
-  const dim3 go(8 * std::min(nbx, 4));  // overflow tiles: rare, few blocks (an empty pass is launch cost only)
-  const dim3 gs(std::max<unsigned>(1, std::min<unsigned>(2048, grid1d(nq, 256))));
-#define KNN_CASE(KK)                                                              \
-  case KK:                                                                        \
-    hipLaunchKernelGGL((k_knn<KK, false>), g, b, 0, s, gp, tstart, rec, tsort,   \
-                       queries, qstart, qperm, idx, dist, lists);                 \
-    hipLaunchKernelGGL((k_knn<KK, true>), go, b, 0, s, gp, tstart, rec, tsort,   \
-                       queries, qstart, qperm, idx, dist, lists);                 \
-    hipLaunchKernelGGL((k_knn_slow<KK>), gs, dim3(256), 0, s, gp, tstart, rec,    \
-                       tsort, queries, idx, dist, lists);                         \
-    break;
-  switch (k) {
-    KNN_CASE(1)
-    KNN_CASE(2)
-    KNN_CASE(3)
-    KNN_CASE(4)
-    KNN_CASE(5)
-    KNN_CASE(6)
-    KNN_CASE(7)
-    KNN_CASE(8)
-    KNN_CASE(9)
-    KNN_CASE(10)
-    KNN_CASE(11)
-    KNN_CASE(12)
-    KNN_CASE(13)
-    KNN_CASE(14)
-    KNN_CASE(15)
-    KNN_CASE(16)
-  }
-#undef KNN_CASE
-  CHECK_LAUNCH("k_knn");
-  return NAVGPU_OK;
-}
-
-extern "C" {
-
-int navgpu_knn_dev(navgpu_ctx *ctx, const double *tgt, size_t nt,
-                   const double *queries, size_t nq, int k, int32_t *idx,
-                   double *dist) {
-  return knn_run(ctx, tgt, nt, queries, nq, k, idx, dist);
-}
-
-int navgpu_knn_host(navgpu_ctx *ctx, const double *tgt, size_t nt,
-                    const double *queries, size_t nq, int k, int32_t *idx,
-                    double *dist) {
-  ARG_CHECK(ctx && k >= 1 && k <= 16);
-  if (!nq) return NAVGPU_OK;
-  ARG_CHECK(queries && idx && dist && (tgt || nt == 0));
-  double *dt = nullptr, *dq, *dd;
-  int32_t *di;
-  if (nt) RC(ws(ctx, kH0, 3 * nt, &dt));
-  RC(ws(ctx, kH1, 3 * nq, &dq));
-  RC(ws(ctx, kH2, nq * k, &di));
-  RC(ws(ctx, kH3, nq * k, &dd));
-  if (nt)
-    HIP_TRY(hipMemcpyAsync(dt, tgt, 24 * nt, hipMemcpyHostToDevice, ctx->stream));
-  HIP_TRY(hipMemcpyAsync(dq, queries, 24 * nq, hipMemcpyHostToDevice, ctx->stream));
-  RC(navgpu_knn_dev(ctx, dt, nt, dq, nq, k, di, dd));
-  HIP_TRY(hipMemcpyAsync(idx, di, 4 * nq * k, hipMemcpyDeviceToHost, ctx->stream));
-  HIP_TRY(hipMemcpyAsync(dist, dd, 8 * nq * k, hipMemcpyDeviceToHost, ctx->stream));
-  HIP_TRY(hipStreamSynchronize(ctx->stream));
-  return NAVGPU_OK;
-}
-
-int navgpu_pair_knn_dev(navgpu_ctx *ctx, const double *src, const double *tgt,
-                        int R, int C, int k, int32_t *src_mask,
-                        int32_t *tgt_mask, int32_t *idx, double *dist) {
-  ARG_CHECK(ctx && R >= 0 && C >= 0);
-  const size_t N = (size_t)R * C;
-  if (!N) return NAVGPU_OK;
-  ARG_CHECK(src && tgt);
-  if (!src_mask && !tgt_mask) return navgpu_knn_dev(ctx, tgt, N, src, N, k, idx, dist);
-  // One curvature launch over both clouds, on a side stream forked from and
-  // joined back into the context's stream: it is f64-bound and independent
-  // of the (latency-bound) index build and query, so the two overlap.
-  if (!ctx->aux) {
-    HIP_TRY(hipStreamCreateWithFlags(&ctx->aux, hipStreamNonBlocking));
-    HIP_TRY(hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming));
-    HIP_TRY(hipEventCreateWithFlags(&ctx->ev_join, hipEventDisableTiming));
-  }
-  CurvJob J = {{src, tgt}, {src_mask, tgt_mask}, {nullptr, nullptr}};
-  if (!src_mask) {  // only the target: it becomes cloud 0
-    J.pts[0] = tgt;
-    J.mask[0] = tgt_mask;
-  }
-  HIP_TRY(hipEventRecord(ctx->ev_fork, ctx->stream));
-  HIP_TRY(hipStreamWaitEvent(ctx->aux, ctx->ev_fork, 0));
-  {
-    TimedRegion tr(ctx, "curvature", ctx->aux);
-    dim3 grid((C + kCurvTile - 1) / kCurvTile, R, (src_mask && tgt_mask) ? 2 : 1);
-    hipLaunchKernelGGL(k_curvature, grid, dim3(kCurvTile), 0, ctx->aux, J, R, C);
-    CHECK_LAUNCH("k_curvature");
-  }
-  HIP_TRY(hipEventRecord(ctx->ev_join, ctx->aux));
-  const int rc = knn_run(ctx, tgt, N, src, N, k, idx, dist);
-  HIP_TRY(hipStreamWaitEvent(ctx->stream, ctx->ev_join, 0));  // join before returning
-  return rc;
 }
 
 }  // extern "C"

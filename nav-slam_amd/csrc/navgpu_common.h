@@ -1,0 +1,242 @@
+// navgpu_common.h — what the two translation units of libnavgpu.so share:
+// navgpu.hip (per-row mode, curvature, KD build, host plumbing) and knn.hip
+// (global-mode grid index and exact k-NN). Internal: never installed.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <math.h>
+#include <stdarg.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <algorithm>
+#include <map>
+#include <string>
+#include <type_traits>
+#include <utility>
+#include <vector>
+
+#include "navgpu.h"
+
+#pragma clang fp contract(off)
+
+constexpr int kWave = 64;
+constexpr int kKnnMaxSx = 8;  // x cells per h of the global-mode grid (knn.hip)
+
+// Diagnostic phase stamps (build with -DNAVGPU_STAMPS; never in the product
+// build): lane 0 of each wave adds s_memtime deltas per phase into g_stamps.
+#ifdef NAVGPU_STAMPS
+// one copy per translation unit (no relocatable device code): navgpu.hip's
+// navgpu_debug_stamps adds knn.hip's through nv::knn_stamps_take
+static __device__ unsigned long long g_stamps[16];
+#define NV_STAMP(v) const unsigned long long v = __builtin_amdgcn_s_memtime()
+#define NV_STAMP_ADD(slot, a, b) \
+  if ((threadIdx.x & 63) == 0) atomicAdd(&g_stamps[slot], (b) - (a))
+#define NV_STAMP_ADD0(slot, a, b) \
+  if (threadIdx.x == 0) atomicAdd(&g_stamps[slot], (b) - (a))
+#define NV_COUNT0(slot) \
+  if (threadIdx.x == 0) atomicAdd(&g_stamps[slot], 1ull)
+// per-wave accumulators, flushed with one atomic per slot at the kernel's end
+// (atomics inside a hot loop would distort what they time)
+#define NV_ACC_DECL unsigned long long nv_acc[16] = {}
+#define NV_ACC(slot, a, b) nv_acc[slot] += (b) - (a)
+#define NV_ACC_FLUSH                                              \
+  if ((threadIdx.x & 63) == 0) {                                  \
+    _Pragma("unroll") for (int s_ = 1; s_ < 16; ++s_)             \
+      if (nv_acc[s_]) atomicAdd(&g_stamps[s_], nv_acc[s_]);       \
+  }
+#else
+#define NV_ACC_DECL
+#define NV_ACC(slot, a, b)
+#define NV_ACC_FLUSH
+#define NV_COUNT0(slot)
+#define NV_STAMP(v)
+#define NV_STAMP_ADD(slot, a, b)
+#define NV_STAMP_ADD0(slot, a, b)
+#endif
+
+namespace nv {
+void set_err(const char *fmt, ...);
+}
+
+#define HIP_TRY(expr)                                                          \
+  do {                                                                         \
+    hipError_t e_ = (expr);                                                    \
+    if (e_ != hipSuccess) {                                                    \
+      nv::set_err("%s:%d %s: %s", __FILE__, __LINE__, #expr,                  \
+                  hipGetErrorString(e_));                                      \
+      return NAVGPU_EHIP;                                                      \
+    }                                                                          \
+  } while (0)
+
+#define CHECK_LAUNCH(name)                                                     \
+  do {                                                                         \
+    hipError_t e_ = hipGetLastError();                                         \
+    if (e_ != hipSuccess) {                                                    \
+      nv::set_err("launch %s: %s", name, hipGetErrorString(e_));              \
+      return NAVGPU_EHIP;                                                      \
+    }                                                                          \
+  } while (0)
+
+#define ARG_CHECK(cond)                                                        \
+  do {                                                                         \
+    if (!(cond)) {                                                             \
+      nv::set_err("invalid argument: %s", #cond);                             \
+      return NAVGPU_EINVAL;                                                    \
+    }                                                                          \
+  } while (0)
+
+#define RC(x)                         \
+  do {                                \
+    int rc_ = (x);                    \
+    if (rc_ != NAVGPU_OK) return rc_; \
+  } while (0)
+
+// ------------------------------------------------------------ device helpers
+namespace {
+
+// utils/kdtree.c:14-17 (euclideanDistance; gcc folds pow(v,2) to v*v) and
+// src/slam.c:28-33,47-50: sqrt((dx*dx + dy*dy) + dz*dz), no contraction.
+__device__ __forceinline__ double ref_dist(double ax, double ay, double az,
+                                           double bx, double by, double bz) {
+  const double dx = ax - bx, dy = ay - by, dz = az - bz;
+  return __builtin_sqrt(dx * dx + dy * dy + dz * dz);
+}
+
+__device__ __forceinline__ int lanes_below(unsigned long long bal) {
+  return __builtin_amdgcn_mbcnt_hi((unsigned)(bal >> 32),
+                                   __builtin_amdgcn_mbcnt_lo((unsigned)bal, 0u));
+}
+
+__device__ __forceinline__ void wave_sync_mem() {
+  // Cross-lane hand-off through memory inside one wavefront (LDS, or global
+  // scratch of the large-n build): workgroup-scope release/acquire makes the
+  // other lanes' stores visible; wave_barrier stops code motion across it.
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+
+// Block-wide exclusive scan of one int per thread. scratch: >= nwaves+1 ints.
+__device__ __forceinline__ int block_excl_scan(int v, int *scratch, int *total) {
+  const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
+  const int nw = blockDim.x / kWave;
+  int incl = v;
+#pragma unroll
+  for (int o = 1; o < kWave; o <<= 1) {
+    int t = __shfl_up(incl, o, kWave);
+    if (lane >= o) incl += t;
+  }
+  if (lane == kWave - 1) scratch[wid] = incl;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int acc = 0;
+    for (int w = 0; w < nw; ++w) {
+      int t = scratch[w];
+      scratch[w] = acc;
+      acc += t;
+    }
+    scratch[nw] = acc;
+  }
+  __syncthreads();
+  const int res = scratch[wid] + incl - v;
+  *total = scratch[nw];
+  __syncthreads();
+  return res;
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------ host
+struct navgpu_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  bool own_stream = false;
+  std::map<int, std::pair<void *, size_t>> bufs;  // grow-only workspace
+  bool timing = false;
+  std::map<std::string, std::vector<std::pair<hipEvent_t, hipEvent_t>>> ev;
+  std::vector<hipEvent_t> free_ev;
+  std::vector<double> tan_c, tan_r;
+  int tan_R = -1, tan_C = -1;
+  hipStream_t aux = nullptr;                 // side stream (pair path: curvature)
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+  double knn_occ = 5.0;  // target points per h^3 grid cell (NAVGPU_KNN_OCC)
+  int knn_sx = 4;        // x cells per h (NAVGPU_KNN_SX)
+  int knn_blocks = 0;    // k_knn blocks per XCD, 0 = auto (NAVGPU_KNN_BLOCKS)
+  double knn_lambda = 22.0;  // expected targets inside a query's first filter radius
+  bool knn_stats = false;
+  int screen_rows = 0, screen_S = 0;  // last screened rows_match call (tie diagnostic)
+};
+
+namespace nv {
+
+// workspace slots (grow-only buffers of a context)
+enum Slot {
+  kBBox = 1, kParams, kCnt, kStart, kBSum, kCellId, kSlotBuf, kRec, kTan,
+  kKdFc, kKdP, kKdT, kQStart, kQCell, kQSlot, kQPerm, kStats, kOvf, kSlowQ,
+  kSlowThr, kTSort, kRowMaskS, kRowMaskT, kRowTie, kCorrEnt, kCorrN, kCorrSums, kKdPtmp, kKdSel,
+  kQSort,
+  kH0 = 100, kH1, kH2, kH3, kH4, kH5,
+};
+
+int ws_get(navgpu_ctx *ctx, int slot, size_t bytes, void **out);
+
+template <class T>
+int ws(navgpu_ctx *ctx, int slot, size_t count, T **out) {
+  void *p;
+  int rc = ws_get(ctx, slot, count * sizeof(T), &p);
+  *out = (T *)p;
+  return rc;
+}
+
+// HIP events around a span of launches on one stream (navgpu_timing_*)
+struct TimedRegion {
+  navgpu_ctx *ctx;
+  const char *name;
+  hipEvent_t a = nullptr, b = nullptr;
+  hipStream_t st;
+  hipEvent_t take() {
+    if (!ctx->free_ev.empty()) {
+      hipEvent_t e = ctx->free_ev.back();
+      ctx->free_ev.pop_back();
+      return e;
+    }
+    hipEvent_t e = nullptr;
+    if (hipEventCreate(&e) != hipSuccess) return nullptr;
+    return e;
+  }
+  TimedRegion(navgpu_ctx *c, const char *n, hipStream_t on = nullptr)
+      : ctx(c), name(n), st(on ? on : c->stream) {
+    if (!ctx->timing) return;
+    a = take();
+    b = take();
+    if (a && b) (void)hipEventRecord(a, st);
+  }
+  ~TimedRegion() {
+    if (!ctx->timing || !a || !b) return;
+    (void)hipEventRecord(b, st);
+    ctx->ev[name].push_back({a, b});
+  }
+};
+
+inline unsigned grid1d(size_t n, int block) {
+  return (unsigned)((n + block - 1) / block);
+}
+
+// diagnostic builds (-DNAVGPU_STAMPS): knn.hip's phase stamps, read and
+// cleared; NAVGPU_EINVAL otherwise
+int knn_stamps_take(unsigned long long *out16);
+
+// side stream of a context, created on first use
+int ensure_aux(navgpu_ctx *ctx);
+
+// R1 curvature of up to two clouds (both R x C, row-major Points) in one
+// launch on `stream` (src/slam.c:11-61); navgpu.hip
+int launch_curvature(const double *pts0, int32_t *mask0, double *curv0,
+                     const double *pts1, int32_t *mask1, double *curv1, int R, int C,
+                     hipStream_t stream);
+
+}  // namespace nv
