@@ -479,9 +479,14 @@ def main():
                     "point, global mode")
         data = (f"synthetic: x,y,z ~ U[0,1000) mm, numpy PCG64 seeds (1+2r+1000j, 2+2r+1000j) "
                 f"on rank r, {npairs} distinct pairs j resident and rotated per step")
+        # under --graph the captured step replays one resident pair
+        res_pairs = 1 if (a.graph and nf == 1) else npairs
+        if res_pairs == 1:
+            data = data.replace(f"{npairs} distinct pairs j resident and rotated per step",
+                                "one resident pair replayed by a hipGraph")
         cfg_extra = {"points_per_cloud": N, "k": a.k, "pairs_per_gpu": 1, "mode": "global",
-                     "pairs_in_flight": nf, "resident_pairs": npairs,
-                     "resident_bytes": npairs * 2 * 24 * N}
+                     "pairs_in_flight": nf, "resident_pairs": res_pairs,
+                     "resident_bytes": res_pairs * 2 * 24 * N}
     else:
         ctxs, iso_step, nf = [g], None, 1
         R = a.rows or 128
@@ -563,7 +568,7 @@ def main():
     # kernel timing on every context; each kernel's average is its summed
     # time over its own launch count (with pairs in flight, a context runs
     # only every nf-th step)
-    names = sorted(set(path_kernels + [dom]))
+    names = sorted(set(path_kernels + [dom] + (["knn_build"] if a.workload == "k3" else [])))
 
     def timing_on(on):
         for c in ctxs:
@@ -655,18 +660,20 @@ def main():
         roof = None
         if dom_bytes is not None and dom_n > 0:
             ach = dom_bytes / (dom_avg_us * 1e-6) / 1e9
-            traffic = None
+            traffic = build_traffic = None
             if a.traffic_csv:
-                traffic = traffic_from_csv(a.traffic_csv.split(","), "k_knn")
+                traffic = traffic_from_csv(a.traffic_csv.split(","))
+                build_traffic = traffic_from_csv(a.traffic_csv.split(","), BUILD_KERNELS)
             elif not a.no_traffic_json and os.path.exists(a.traffic_json):
                 with open(a.traffic_json) as f:
                     tj = json.load(f)
                 if tj.get("k") == a.k and tj.get("points_per_cloud") == N:
                     traffic = tj.get("bytes_per_step")
+                    build_traffic = tj.get("build_bytes_per_step")
             roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
                     "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic,
-                    "kernel": ("query stage k_knn<%d,false> + k_knn<%d,true> (overflow tiles) "
-                               "+ k_knn_slow<%d>, one launch each per step" % (a.k, a.k, a.k)),
+                    "kernel": ("query stage k_knn<%d> + k_knn_slow<%d>, one launch each per "
+                               "step" % (a.k, a.k)),
                     "avg_us": round(dom_avg_us, 2), "launches": dom_n,
                     "timing": ("HIP events on each context's stream over the timed region"
                                + (f" ({nf} pairs in flight: shares the chip with the other "
@@ -677,6 +684,20 @@ def main():
                 iso_us = 1000.0 * kt_iso[dom][0] / kt_iso[dom][1]
                 roof["avg_us_isolated"] = round(iso_us, 2)
                 roof["frac_isolated"] = round(dom_bytes / (iso_us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)
+            # the index build is reported separately, outside the
+            # headline fraction: its time, the 24 B/target read of the model
+            # and its measured traffic
+            b_ms, b_n = kt.get("knn_build", (0.0, 0))
+            if b_n:
+                bld = {"kernels": ("k_bbox_partial + k_grid_params + k_bin_hist + k_scan_sums + "
+                                   "k_scan_apply + k_bin_scatter + k_bin_fine (both clouds binned)"),
+                       "avg_us": round(1000.0 * b_ms / b_n, 2),
+                       "bytes_model": "24 B/target read (SURVEY 8d); the query binning is extra",
+                       "algorithmic_bytes": 24 * N, "traffic": build_traffic}
+                if kt_iso is not None and kt_iso.get("knn_build", (0, 0))[1] > 0:
+                    bld["avg_us_isolated"] = round(
+                        1000.0 * kt_iso["knn_build"][0] / kt_iso["knn_build"][1], 2)
+                roof["build"] = bld
         elif dom_n > 0:
             roof = {"bound": "hbm", "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": None, "traffic": None, "kernel": dom,
@@ -749,12 +770,18 @@ def main():
     return out
 
 
-def traffic_from_csv(paths, kernel_sub):
-    """HBM bytes per step of the kernels whose name contains `kernel_sub`, from
-    rocprofv3 --pmc counter CSVs (FETCH_SIZE in one pass, WRITE_SIZE in another;
-    both in KB). FETCH_SIZE is doubled on gfx950 (MI355X_MICROARCH.md, HBM
-    section). Per step = total / launches of the main query kernel
-    (k_knn<..., false>), the other query-stage kernels being part of the step."""
+QUERY_KERNELS = ("k_knn<", "k_knn_slow<")
+BUILD_KERNELS = ("k_bbox_partial", "k_grid_params", "k_bin_hist", "k_scan_sums",
+                 "k_scan_apply", "k_bin_scatter", "k_bin_fine")
+
+
+def pmc_bytes(paths, kernel_subs):
+    """HBM bytes per K3 step of the kernels whose name contains one of
+    `kernel_subs`, from rocprofv3 --pmc counter CSVs (FETCH_SIZE in one pass,
+    WRITE_SIZE in another; both in KB). Per step = total / launches of the
+    query kernel k_knn<K> (one per step). Returns {"fetch_raw", "write",
+    "bytes"}: FETCH_SIZE as counted, WRITE_SIZE, and FETCH_SIZE x 2 (the
+    gfx950 correction, MI355X_MICROARCH.md HBM section) + WRITE_SIZE."""
     import csv
     fetch, write = 0.0, 0.0
     launches = {}
@@ -762,22 +789,26 @@ def traffic_from_csv(paths, kernel_sub):
         with open(path) as f:
             for r in csv.DictReader(f):
                 name = r.get("Kernel_Name", "")
-                if kernel_sub not in name:
+                c = r.get("Counter_Name")
+                if "k_knn<" in name:
+                    launches.setdefault(c, set()).add(r.get("Dispatch_Id"))
+                if not any(k in name for k in kernel_subs):
                     continue
                 v = float(r.get("Counter_Value", 0))
-                c = r.get("Counter_Name")
                 if c == "FETCH_SIZE":
                     fetch += v
                 elif c == "WRITE_SIZE":
                     write += v
-                else:
-                    continue
-                if "false>" in name:
-                    launches.setdefault(c, set()).add(r.get("Dispatch_Id"))
     nf, nw = len(launches.get("FETCH_SIZE", ())), len(launches.get("WRITE_SIZE", ()))
     if not nf or not nw:
         return None
-    return round((2 * fetch / nf + write / nw) * 1024)
+    return {"fetch_raw": round(fetch / nf * 1024), "write": round(write / nw * 1024),
+            "bytes": round((2 * fetch / nf + write / nw) * 1024)}
+
+
+def traffic_from_csv(paths, kernel_subs=QUERY_KERNELS):
+    t = pmc_bytes(paths, kernel_subs)
+    return None if t is None else t["bytes"]
 
 
 if __name__ == "__main__":

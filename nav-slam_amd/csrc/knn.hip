@@ -14,8 +14,11 @@
 //                                   h/sx x h x h, ~occ targets per h^3)
 //   k_bin_hist, k_scan_*, k_bin_scatter, k_bin_fine
 //                                   both clouds counting-sorted by cell
-//                                   (LDS atomics only), written as 32-B
-//                                   records (f64 point, index, x column)
+//                                   (LDS atomics only): the targets as
+//                                   cell-sorted 32-B records (f64 point,
+//                                   index, x column), the queries as a
+//                                   cell-sorted permutation (4 B) of their
+//                                   coarse-bucketed records
 //   k_knn<K>                        tiles of one grid row: the 9 neighbouring
 //                                   row segments staged in LDS (column-major),
 //                                   one query per lane: packed-f32 screen,
@@ -56,6 +59,12 @@ struct __align__(16) PRec {
 
 // ---- k_knn tile geometry (LDS budget: 4 blocks of 192 threads per CU)
 constexpr int kTileThreads = 192;  // 3 waves: a ~145-query tile fills them
+// waves per SIMD k_knn's registers must allow: 5 blocks of 3 waves per CU
+// (the LDS limit) need 4, i.e. <= 128 VGPRs
+#ifndef NAVGPU_KNN_MINW
+#define NAVGPU_KNN_MINW 4
+#endif
+constexpr int kKnnMinWaves = NAVGPU_KNN_MINW;
 constexpr int kTileRec = 1568;     // staged records per tile (16 B each)
 constexpr int kTilePairs = kTileRec / 2 + 2;  // two spare pairs: read-ahead
 constexpr int kZgOff = 4 * kTilePairs;        // floats from the XY plane to the ZG plane
@@ -69,11 +78,15 @@ constexpr double kTileQueries = 150.0;  // target queries per tile
 #endif
 constexpr bool kList = NAVGPU_KNN_LIST;
 constexpr int kListCap = 12;       // survivors a lane holds before a drain
+#ifndef NAVGPU_KNN_PREFETCH
+#define NAVGPU_KNN_PREFETCH 1
+#endif
+constexpr bool kPrefetch = NAVGPU_KNN_PREFETCH;  // pipelined LDS reads in the scan
 constexpr int kKeyBits = 8;        // local id in the low bits of a packed key
 constexpr uint32_t kKeyMask = (1u << kKeyBits) - 1;
 constexpr uint32_t kNoKey = 0xffffffffu;
 
-constexpr int kBBoxBlocks = 1024;
+constexpr int kBBoxBlocks = 256;  // bbox partials (every k_bin_hist block reduces them)
 
 // Timing-only ablations of k_knn (never in the product build: -DNAVGPU_ABL=...
 // in scripts/build_variants.sh); the results are wrong in such builds.
@@ -135,6 +148,7 @@ __global__ __launch_bounds__(256) void k_grid_params(const double *__restrict__ 
                                                      GridParams *gp, int *counters) {
   // also resets the call's k-NN counters (one launch fewer than a memset)
   if (threadIdx.x < 4) counters[threadIdx.x] = 0;
+  GridParams *out = gp;
   __shared__ double s[4][6];
   double v6[6] = {INFINITY, INFINITY, INFINITY, -INFINITY, -INFINITY, -INFINITY};
   for (int b = threadIdx.x; b < nparts; b += blockDim.x)
@@ -173,7 +187,7 @@ __global__ __launch_bounds__(256) void k_grid_params(const double *__restrict__ 
     G.ncells = 1;
     G.tile_w = 1;
     G.clamped = 0;
-    *gp = G;
+    *out = G;
     return;
   }
   const double emax = fmax(ext[0], fmax(ext[1], ext[2]));
@@ -224,7 +238,7 @@ __global__ __launch_bounds__(256) void k_grid_params(const double *__restrict__ 
   const int wmax = (int)fmax(1.0, fmin((double)(kTileCols - 1 - 2 * sx), floor(w)));
   const int tpr = (G.g[0] + wmax - 1) / wmax;
   G.tile_w = (G.g[0] + tpr - 1) / tpr;
-  *gp = G;
+  *out = G;
 }
 
 __device__ __forceinline__ int cell_axis(double v, const GridParams &G, int a) {
@@ -289,12 +303,16 @@ __global__ __launch_bounds__(kScanBlock) void k_scan_apply(const int *__restrict
 //                bucket-major table[b * nblk + block], so ONE exclusive scan
 //                of the table gives every (bucket, block) its output offset.
 //  k_bin_scatter same chunks: each point gets an LDS rank within its
-//                (bucket, block) and moves to the coarse-bucketed array.
+//                (bucket, block) and moves to the coarse-bucketed array
+//                (BinPt, 32 B).
 //  k_bin_fine    one block per bucket: LDS counting sort over the bucket's
-//                2^shift cells, writes start[] for them and every point at its
-//                final cell-sorted position as a PRec. Order inside a cell is
-//                unspecified: the k-NN result does not depend on it (ties are
-//                resolved by (distance, index) in the exact stage).
+//                2^shift cells, writes start[] for them; targets: every point
+//                at its final cell-sorted position as a PRec (k_knn stages
+//                row segments of them, coalesced); queries: only the
+//                permutation qperm[g] = the bucketed position (k_knn reads a
+//                tile's queries from one or two buckets: L2-local gathers).
+//                Order inside a cell is unspecified: the k-NN result does not
+//                depend on it (ties are resolved by (distance, index)).
 // Side 0 = targets, side 1 = queries; both go through the same launches
 // (block ranges) and their tables are concatenated so one scan covers both.
 struct BinPt {
@@ -307,8 +325,9 @@ struct BinSide {
   int tab;  // offset of this side's table in the concatenated table
   int sub;  // subtracted from scanned offsets (targets' total, for side 1)
   int *start;
-  BinPt *bin;   // coarse-bucketed
-  PRec *sorted; // cell-sorted
+  BinPt *bin;    // coarse-bucketed points
+  PRec *sorted;  // targets: cell-sorted records
+  int *perm;     // queries: cell-sorted position -> bucketed position
 };
 struct BinJob {
   BinSide s[2];
@@ -389,9 +408,10 @@ __global__ __launch_bounds__(256) void k_bin_scatter(BinJob J, const GridParams 
 }
 
 // One bucket: count its points per cell (LDS), scan, write the cell starts,
-// then place every point. The first kBinFineHold * blockDim points stay in
-// registers between the count and the placement (one global read, not two);
-// a larger bucket re-reads the rest.
+// then place every point (targets) or its bucketed position (queries). The
+// first kBinFineHold * blockDim points stay in registers between the count
+// and the placement (one global read, not two); a larger bucket re-reads the
+// rest.
 __global__ __launch_bounds__(kBinFineThreads) void k_bin_fine(BinJob J,
                                                               const GridParams *__restrict__ gp,
                                                               const int *__restrict__ offs,
@@ -407,12 +427,18 @@ __global__ __launch_bounds__(kBinFineThreads) void k_bin_fine(BinJob J,
   const BinPt *src = S.bin;
   for (int j = threadIdx.x; j < ncell; j += blockDim.x) cnt[j] = 0;
   __syncthreads();
+  // queries hold only their cell (the placement writes the position)
   BinPt hold[kBinFineHold];
   const int bd = (int)blockDim.x, held_end = min(hi, lo + kBinFineHold * bd);
 #pragma unroll
   for (int u = 0; u < kBinFineHold; ++u) {
     const int i = lo + u * bd + (int)threadIdx.x;
-    if (i < held_end) hold[u] = src[i];
+    if (i < held_end) {
+      if (side)
+        hold[u].cell = src[i].cell;
+      else
+        hold[u] = src[i];
+    }
   }
 #pragma unroll
   for (int u = 0; u < kBinFineHold; ++u) {
@@ -436,22 +462,26 @@ __global__ __launch_bounds__(kBinFineThreads) void k_bin_fine(BinJob J,
   }
   __syncthreads();
   const int g0 = gp->g[0];
-  auto place = [&](const BinPt &e) {
+  auto place = [&](const BinPt &e, int i) {
     const int pos = atomicAdd(&cnt[e.cell - base], 1);
-    PRec t;
-    t.x = e.x;
-    t.y = e.y;
-    t.z = e.z;
-    t.idx = e.idx;
-    t.cx = e.cell % g0;
-    S.sorted[pos] = t;
+    if (side) {
+      S.perm[pos] = i;
+    } else {
+      PRec t;
+      t.x = e.x;
+      t.y = e.y;
+      t.z = e.z;
+      t.idx = e.idx;
+      t.cx = e.cell % g0;
+      S.sorted[pos] = t;
+    }
   };
 #pragma unroll
   for (int u = 0; u < kBinFineHold; ++u) {
     const int i = lo + u * bd + (int)threadIdx.x;
-    if (i < held_end) place(hold[u]);
+    if (i < held_end) place(hold[u], i);
   }
-  for (int i = held_end + (int)threadIdx.x; i < hi; i += bd) place(src[i]);
+  for (int i = held_end + (int)threadIdx.x; i < hi; i += bd) place(src[i], i);
 }
 
 // ============================================================ k-NN helpers
@@ -510,19 +540,25 @@ __device__ __forceinline__ double block_reach(const GridParams &G, const double 
   return L;
 }
 
+// sqrt(v) rounded up by more than v_sqrt_f32's 1-ulp error: an upper bound
+// for the error terms below (they only need to bound, not be exact)
+__device__ __forceinline__ double sqrt_up(double v) {
+  return (double)__builtin_amdgcn_sqrtf((float)v) * (1.0 + 0x1p-20);
+}
+
 // Error of the packed-f32 squared distance: each coordinate is rounded to f32
 // once relative to the tile origin (<= 2^-24 |v|) and subtracted once in f32,
 // so each difference is within dl = Dq 2^-22 of the exact one (Dq bounds the
 // magnitudes); then |d2_f32 - d2| <= err(d2_f32-ish) below.
 __device__ __forceinline__ double f32_err(double V, double dl) {
-  return V * 0x1p-20 + 4.0 * dl * __builtin_sqrt(V) + 4.0 * dl * dl;
+  return V * 0x1p-20 + 4.0 * dl * sqrt_up(V) + 4.0 * dl * dl;
 }
 
 // f32 admission bound for an f64 dsq bound T: every candidate whose exact
 // dsq is <= T has an f32 dsq <= the returned value.
 __device__ __forceinline__ float f32_bound(double T, double dl) {
   if (!(T < INFINITY)) return INFINITY;
-  const double E = T * 0x1p-20 + 4.0 * dl * __builtin_sqrt(T) + 4.0 * dl * dl;
+  const double E = T * 0x1p-20 + 4.0 * dl * sqrt_up(T) + 4.0 * dl * dl;
   return (float)((T + E) * (1.0 + 0x1p-20));
 }
 
@@ -589,11 +625,11 @@ __device__ __forceinline__ void push_slow(const KnnLists &L_, int qi, double thr
 // that bound exceeds the K-th exact dsq (times 1 + 2^-46), the answer is
 // exact; otherwise the query goes to k_knn_slow with the K-th dsq as bound.
 template <int K>
-__global__ __launch_bounds__(kTileThreads, 4) void k_knn(
+__global__ __launch_bounds__(kTileThreads, kKnnMinWaves) void k_knn(
     const GridParams *__restrict__ gp, const int *__restrict__ tstart,
     const PRec *__restrict__ tsort, const int *__restrict__ qstart,
-    const PRec *__restrict__ qsort, int32_t *__restrict__ oidx, double *__restrict__ odist,
-    KnnLists L_, float lambda) {
+    const BinPt *__restrict__ qbin, const int *__restrict__ qperm, int32_t *__restrict__ oidx,
+    double *__restrict__ odist, KnnLists L_, float lambda) {
   __shared__ __attribute__((aligned(16))) float spair[2 * kZgOff];
   // cbr[r][j]: the LDS slot of the record at cell-sorted position g of cell
   // (row r, tile column j) is cbr[r][j] + g - sbase. Before that: the row
@@ -739,10 +775,11 @@ __global__ __launch_bounds__(kTileThreads, 4) void k_knn(
       const int q0 = qstart[cell0 + qa], q1 = qstart[cell0 + qb + 1];
       for (int qi = q0 + tid; qi < q1 && !(kAbl & kAblNoQuery); qi += kTileThreads) {
         NV_STAMP(ts0);
-        const PRec Q = qsort[qi];
+        const BinPt Q = qbin[qperm[qi]];
         const double qv[3] = {Q.x, Q.y, Q.z};
-        const int c[3] = {Q.cx, y, z};
-        const int i = Q.cx - (xa - S);  // tile column of the query's cell
+        const int qcx = Q.cell - (z * G.g[1] + y) * G.g[0];  // the cell's x index
+        const int c[3] = {qcx, y, z};
+        const int i = qcx - (xa - S);  // tile column of the query's cell
         const int t0 = colst[i - S] - sbase, t1 = colst[i + S + 1] - sbase;
         const double qr[3] = {qv[0] - ot[0], qv[1] - ot[1], qv[2] - ot[2]};
         const double Dq = fmax(Dt, fmax(fabs(qr[0]), fmax(fabs(qr[1]), fabs(qr[2]))));
@@ -830,14 +867,37 @@ __global__ __launch_bounds__(kTileThreads, 4) void k_knn(
         if (np > 2) {
           const float *last = spair + ((ta >> 1) + np - 1) * 4;
           uint32_t v2 = 2;
-          do {
-            const f2 d = dist2(cur);
-            offer(knn_key(d[0], vmask, v2));
-            offer(knn_key(d[1], vmask, v2 + 1));
-            cur += 4;
-            v2 += 2;
-            if (__any(nearly_full())) drain();
-          } while (cur < last);
+          if constexpr (kPrefetch) {
+            // software-pipelined: the next pair's LDS reads are issued before
+            // this pair's arithmetic (the read past the block's last interior
+            // pair lands on its last pair or a spare one)
+            float4 xy = *(const float4 *)cur;
+            float2 zz = *(const float2 *)(cur + kZgOff);
+            do {
+              const float4 nxy = *(const float4 *)(cur + 4);
+              const float2 nzz = *(const float2 *)(cur + 4 + kZgOff);
+              const f2 fx2 = f2{xy.x, xy.y} - qx2, fy2 = f2{xy.z, xy.w} - qy2,
+                       fz2 = f2{zz.x, zz.y} - qz2;
+              const f2 d = __builtin_elementwise_fma(
+                  fz2, fz2, __builtin_elementwise_fma(fy2, fy2, fx2 * fx2));
+              offer(knn_key(d[0], vmask, v2));
+              offer(knn_key(d[1], vmask, v2 + 1));
+              cur += 4;
+              v2 += 2;
+              xy = nxy;
+              zz = nzz;
+              if (__any(nearly_full())) drain();
+            } while (cur < last);
+          } else {
+            do {
+              const f2 d = dist2(cur);
+              offer(knn_key(d[0], vmask, v2));
+              offer(knn_key(d[1], vmask, v2 + 1));
+              cur += 4;
+              v2 += 2;
+              if (__any(nearly_full())) drain();
+            } while (cur < last);
+          }
         }
         if (np > 1) {  // last pair: may end past the block
           const f2 d = dist2(cur);
@@ -851,31 +911,21 @@ __global__ __launch_bounds__(kTileThreads, 4) void k_knn(
         }
         drain();
         NV_STAMP(ts2);
-        // ---- certificate bound on every candidate left out
-        double B = INFINITY;
-        if (Lr < INFINITY) {
-          const double Lg = Lr - 2.0 * G.delta;
-          B = Lg > 0.0 ? Lg * Lg : 0.0;
-        }
-        B = fmin(B, Tgeo);  // rejected against the first threshold: exact dsq > Tgeo
-        if (key[K] != kNoKey) {
-          const double V = (double)__uint_as_float(key[K] & vmask);
-          B = fmin(B, V - f32_err(V, dl));
-        }
         bool ok = !overflow && Dq < 1e17;
         if (kAbl & kAblNoExact) {  // timing-only: keep the keys live, one store
           uint32_t acc = 0;
 #pragma unroll
           for (int s = 0; s < KL; ++s) acc ^= key[s];
-          oidx[(size_t)Q.idx * K] = (int)acc + (int)B;
+          oidx[(size_t)Q.idx * K] = (int)acc + (int)ok;
           continue;
         }
-        // ---- exact f64 stage on the K best keys. All loads are issued
-        // unconditionally (an empty slot re-reads slot 0) so their latencies
-        // overlap; coordinates from the cell-sorted copy (L2-local).
+        // ---- exact f64 stage on the K best keys (none if the block was
+        // empty: then no slot is staged). All loads are issued unconditionally
+        // (an empty slot re-reads slot 0) so their latencies overlap;
+        // coordinates from the cell-sorted copy (L2-local).
         double ed[K];
         int ei[K];
-        {
+        if (key[0] != kNoKey) {
           int gpos[K];
 #pragma unroll
           for (int s = 0; s < K; ++s) {
@@ -886,12 +936,13 @@ __global__ __launch_bounds__(kTileThreads, 4) void k_knn(
           }
 #pragma unroll
           for (int s = 0; s < K; ++s) {
-            const bool val = key[s] != kNoKey && count > 0;
-            // x, y as one 16-B load, z and idx as an 8-B and a 4-B load
+            const bool val = key[s] != kNoKey;
+            // the 32-B record as two 16-B loads: (x, y) and (z, idx | cx)
             const PRec *tp = tsort + gpos[s];
             const double2 xy = *(const double2 *)&tp->x;
-            const double pz = tp->z;
-            const int pid = tp->idx;
+            const double2 zi = *(const double2 *)&tp->z;
+            const double pz = zi.x;
+            const int pid = __double2loint(zi.y);
             const double ddx = xy.x - qv[0], ddy = xy.y - qv[1], ddz = pz - qv[2];
             const double dsq = ddx * ddx + ddy * ddy + ddz * ddz;  // utils/kdtree.c:16
             ei[s] = val ? pid : -1;
@@ -903,6 +954,23 @@ __global__ __launch_bounds__(kTileThreads, 4) void k_knn(
               ok = false;
             }
           }
+        } else {
+#pragma unroll
+          for (int s = 0; s < K; ++s) {
+            ed[s] = INFINITY;
+            ei[s] = -1;
+          }
+        }
+        // ---- certificate bound on every candidate left out
+        double B = INFINITY;
+        if (Lr < INFINITY) {
+          const double Lg = Lr - 2.0 * G.delta;
+          B = Lg > 0.0 ? Lg * Lg : 0.0;
+        }
+        B = fmin(B, Tgeo);  // rejected against the first threshold: exact dsq > Tgeo
+        if (key[K] != kNoKey) {
+          const double V = (double)__uint_as_float(key[K] & vmask);
+          B = fmin(B, V - f32_err(V, dl));
         }
         // order by (distance, index): the truncated-key order is almost always
         // right and a misordered survivor sits next to its place; bubble
@@ -1046,7 +1114,8 @@ template <int K>
 __global__ __launch_bounds__(256) void k_knn_slow(const GridParams *__restrict__ gp,
                                                   const int *__restrict__ start,
                                                   const PRec *__restrict__ tsort,
-                                                  const PRec *__restrict__ qsort,
+                                                  const BinPt *__restrict__ qbin,
+                                                  const int *__restrict__ qperm,
                                                   int32_t *__restrict__ oidx,
                                                   double *__restrict__ odist, KnnLists L_) {
   __shared__ double sd[4][kWave];  // per-wave survivor buffers (256 threads)
@@ -1058,7 +1127,7 @@ __global__ __launch_bounds__(256) void k_knn_slow(const GridParams *__restrict__
   const int nwaves = (int)(gridDim.x * blockDim.x / kWave);
   const int gmax = max((G.g[0] + G.sx - 1) / G.sx, max(G.g[1], G.g[2]));
   for (int e = wave; e < n; e += nwaves) {
-    const PRec Q = qsort[L_.slow_q[e]];
+    const BinPt Q = qbin[qperm[L_.slow_q[e]]];
     const size_t q = (size_t)Q.idx;
     double thr = L_.slow_thr[e];
     const double qv[3] = {Q.x, Q.y, Q.z};
@@ -1273,8 +1342,9 @@ static int knn_run(navgpu_ctx *ctx, const double *tgt, size_t nt, const double *
   double *part;
   GridParams *gp;
   int *tab, *offs, *tstart, *qstart, *bsum, *counters;
-  BinPt *bin_t = nullptr, *bin_q;
-  PRec *tsort = nullptr, *qsort;
+  BinPt *tbin = nullptr, *qbin;
+  PRec *tsort = nullptr;
+  int *qperm;
   RC(ws(ctx, kBBox, (size_t)kBBoxBlocks * 6, &part));
   RC(ws(ctx, kParams, 1, &gp));
   RC(ws(ctx, kCnt, (size_t)ntab, &tab));
@@ -1284,19 +1354,21 @@ static int knn_run(navgpu_ctx *ctx, const double *tgt, size_t nt, const double *
   RC(ws(ctx, kBSum, nbs, &bsum));
   RC(ws(ctx, kStats, 4, &counters));  // zeroed by k_grid_params
   if (nt) {
-    RC(ws(ctx, kSlotBuf, nt, &bin_t));
+    RC(ws(ctx, kSlotBuf, nt, &tbin));
     RC(ws(ctx, kTSort, nt, &tsort));
   }
-  RC(ws(ctx, kQCell, nq, &bin_q));
-  RC(ws(ctx, kQSort, nq, &qsort));
+  RC(ws(ctx, kQCell, nq, &qbin));
+  RC(ws(ctx, kQPerm, nq, &qperm));
   J.s[0].p = tgt;
   J.s[1].p = queries;
   J.s[0].start = tstart;
   J.s[1].start = qstart;
-  J.s[0].bin = bin_t;
-  J.s[1].bin = bin_q;
+  J.s[0].bin = tbin;
+  J.s[1].bin = qbin;
   J.s[0].sorted = tsort;
-  J.s[1].sorted = qsort;
+  J.s[1].sorted = nullptr;
+  J.s[0].perm = nullptr;
+  J.s[1].perm = qperm;
   hipStream_t s = ctx->stream;
   {
     TimedRegion tb(ctx, "knn_build");
@@ -1343,10 +1415,10 @@ static int knn_run(navgpu_ctx *ctx, const double *tgt, size_t nt, const double *
   const float lambda = (float)ctx->knn_lambda;
 #define KNN_CASE(KK)                                                                        \
   case KK:                                                                                  \
-    hipLaunchKernelGGL((k_knn<KK>), g, b, 0, s, gp, tstart, tsort, qstart, qsort, idx, dist, \
-                       lists, lambda);                                                      \
-    hipLaunchKernelGGL((k_knn_slow<KK>), gs, dim3(256), 0, s, gp, tstart, tsort, qsort, idx, \
-                       dist, lists);                                                        \
+    hipLaunchKernelGGL((k_knn<KK>), g, b, 0, s, gp, tstart, tsort, qstart, qbin, qperm, idx,  \
+                       dist, lists, lambda);                                                \
+    hipLaunchKernelGGL((k_knn_slow<KK>), gs, dim3(256), 0, s, gp, tstart, tsort, qbin, qperm, \
+                       idx, dist, lists);                                                   \
     break;
   switch (k) {
     KNN_CASE(1)

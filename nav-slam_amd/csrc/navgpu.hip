@@ -2531,6 +2531,11 @@ int navgpu_rows_corr_dev(navgpu_ctx *ctx, const double *tree_pts,
   int HS = 64;
   while (HS < 2 * C) HS <<= 1;
   const int lds = HS * (8 + 4 + 4 + 4) + 4 * C;
+  if (lds > lds_limit()) {
+    set_err("rows_corr: C=%d needs %d B of LDS (device limit %d; C <= 2048 fits)", C, lds,
+            lds_limit());
+    return NAVGPU_ERANGE;
+  }
   RC(set_lds(k_rows_corr, lds));
   TimedRegion tr(ctx, "rows_corr");
   hipLaunchKernelGGL(k_rows_corr, dim3(R), dim3(kCorrBlock), lds, ctx->stream, tree_pts,
@@ -2557,6 +2562,11 @@ int navgpu_rows_corr_list_dev(navgpu_ctx *ctx, const double *tree_pts,
   int HS = 64;
   while (HS < 2 * C) HS <<= 1;
   const int lds = HS * (8 + 4 + 4 + 4) + 4 * C;
+  if (lds > lds_limit()) {
+    set_err("rows_corr: C=%d needs %d B of LDS (device limit %d; C <= 2048 fits)", C, lds,
+            lds_limit());
+    return NAVGPU_ERANGE;
+  }
   double *ent, *sums;
   int32_t *ent_n;
   RC(ws(ctx, kCorrEnt, 7 * (size_t)R * C, &ent));
@@ -2749,8 +2759,17 @@ int navgpu_kd_build_dev(navgpu_ctx *ctx, double *pts, size_t n, int depth0) {
                           // scatter follows whatever is left
   int32_t *stbuf;
   const int nWmax = 1 << std::max(0, L - 1);
-  const int nbmax = (int)((n + kSelChunk - 1) / kSelChunk);
-  RC(ws(ctx, kKdSel, (size_t)7 * nWmax + (size_t)nWmax * nbmax + kRounds + 1, &stbuf));
+  // the selection kernels put a level's windows on grid.y
+  if (nWmax > 65535) {
+    set_err("kd_build: %zu points need %d windows per level (grid.y limit 65535)", n, nWmax);
+    return NAVGPU_ERANGE;
+  }
+  // per-level chunk counters: nW windows x chunks of one window, at most
+  // about n / kSelChunk + nW at any level (not nWmax x all chunks of n)
+  size_t ncnt = 0;
+  for (int d = 0; d < L; ++d)
+    ncnt = std::max(ncnt, ((size_t)1 << d) * (((n >> d) + kSelChunk - 1) / kSelChunk));
+  RC(ws(ctx, kKdSel, (size_t)7 * nWmax + ncnt + kRounds + 1, &stbuf));
   for (int d = 0; d < L; ++d) {
     const int nW = 1 << d;
     const int maxlen = (int)(n >> d);
@@ -2791,7 +2810,7 @@ int navgpu_kd_build_dev(navgpu_ctx *ctx, double *pts, size_t n, int depth0) {
       hipLaunchKernelGGL(k_sel_scatter, grid, dim3(kSelThreads), 0, ctx->stream, st, P, Ptmp, T);
       hipLaunchKernelGGL(k_sel_update, dim3(1), dim3(256), 0, ctx->stream, st, kRounds);
       CHECK_LAUNCH("k_sel");
-      if (it > 4 * ni + 64) {  // quickselect shrinks its window every iteration
+      if ((long long)it > 4LL * ni + 64) {  // quickselect shrinks its window every iteration
         set_err("kd_build: selection did not converge (level %d)", d);
         return NAVGPU_EHIP;
       }

@@ -178,7 +178,7 @@ enum Slot {
   kBBox = 1, kParams, kCnt, kStart, kBSum, kCellId, kSlotBuf, kRec, kTan,
   kKdFc, kKdP, kKdT, kQStart, kQCell, kQSlot, kQPerm, kStats, kOvf, kSlowQ,
   kSlowThr, kTSort, kRowMaskS, kRowMaskT, kRowTie, kCorrEnt, kCorrN, kCorrSums, kKdPtmp, kKdSel,
-  kQSort,
+  kQSort, kCellId2,
   kH0 = 100, kH1, kH2, kH3, kH4, kH5,
 };
 
