@@ -202,6 +202,35 @@ def test_rows_match_batch_equals_per_pair(gpu, orc):
             _eq(x, y, f"pair {p} {name}")
 
 
+def test_rows_match_batch_k4_full_size(gpu):
+    """K4 at full size, as bench.py --workload k4 builds it: 256 pairs of
+    128 x 2048 (8 distinct L9-shaped pairs, seeds 5..12, cycled; here pair 3
+    of every 8 is integer-mm, L9's native format) in ONE batch launch of
+    rows_match_batch_dev, every pair compared with the single-pair rows_match
+    of the same clouds (which the reference digests pin,
+    test_rows_match_k2_matches_reference_digest)."""
+    import torch
+    from navslam.synth import l9_pair
+    R, Cc, P, ND = 128, 2048, 256, 8
+    distinct = [l9_pair(R, Cc, seed=p + 5, integer_mm=p == 3) for p in range(ND)]
+    dev = torch.device("cuda", 0)
+    src = torch.stack([torch.from_numpy(distinct[p % ND][0]) for p in range(P)]).to(dev)
+    tgt = torch.stack([torch.from_numpy(distinct[p % ND][1]) for p in range(P)]).to(dev)
+    i32 = lambda: torch.full((P, R, Cc), -7, dtype=torch.int32, device=dev)  # noqa: E731
+    sm, tm, idx = i32(), i32(), i32()
+    dist = torch.zeros((P, R, Cc), dtype=torch.float64, device=dev)
+    gpu.rows_match_batch_dev(src, tgt, P, R, Cc, sm, tm, idx, dist)
+    torch.cuda.synchronize()
+    del src, tgt
+    singles = [gpu.rows_match(a, b) for a, b in distinct]
+    assert (singles[3][2] >= 0).sum() > 100000  # the integer-mm pair has work
+    names = ("src_mask", "tgt_mask", "nn_idx", "nn_dist")
+    got_all = [t.cpu().numpy() for t in (sm, tm, idx, dist)]
+    for p in range(P):
+        for x, y, name in zip(got_all, singles[p % ND], names):
+            _eq(x[p], y, f"pair {p} {name}")
+
+
 def test_rows_match_batch_lean_path(gpu, orc, monkeypatch):
     """A batch of >= 1024 rows takes the lean two-rows-per-CU kernel
     (k_rows_match_lean): same masks, indices and distances as the oracle and
