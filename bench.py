@@ -59,6 +59,9 @@ def parse():
     p.add_argument("--rows", type=int, default=None)
     p.add_argument("--cols", type=int, default=None)
     p.add_argument("--pairs", type=int, default=256, help="k4: total pairs")
+    p.add_argument("--integer-mm", action="store_true",
+                   help="k2/k4: coordinates rounded to whole mm (the tie-heavy case: rows "
+                        "with equidistant targets take the reference tree)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--graph", action="store_true",
                    help="k3: capture one step into a hipGraph and replay it")
@@ -97,7 +100,7 @@ def dist_env():
 
 
 def host_info():
-    """nproc, the CPU model and the threads the all-cores legs may use."""
+    """nproc, the CPU model and the threads the multi-thread legs use."""
     model = None
     try:
         with open("/proc/cpuinfo") as f:
@@ -152,7 +155,8 @@ def cpu_baseline_k3(src, tgt, k, reps):
     (src/slam.c:11-61) on both 512x2048 clouds (the reference's own is fixed
     to 8x8). Two legs, each the median of `reps` after one warm-up:
       1 core    : as the reference runs (single-threaded);
-      all cores : OpenMP over the queries (the search only reads the tree)
+      threads_N : OpenMP over the queries on N threads (the search only reads
+                  the tree; N = OMP_NUM_THREADS, 16 on the GPU box)
                   and over rows for the curvature; the tree build is the
                   reference's serial recursion.
     """
@@ -189,10 +193,11 @@ def cpu_baseline_k3(src, tgt, k, reps):
     tall, tsall = median_after_warmup(run(threads), reps)
     return {"value": round(N / t1, 1), "unit": "matches/s", "cores": 1, "kind": kind,
             "seconds_per_pair": round(t1, 4), "runs_s": [round(t, 4) for t in ts1],
-            "all_cores": {"value": round(N / tall, 1), "unit": "matches/s", "cores": threads,
-                          "seconds_per_pair": round(tall, 4),
-                          "runs_s": [round(t, 4) for t in tsall],
-                          "note": "OpenMP over queries and curvature rows; serial tree build"},
+            f"threads_{threads}": {"value": round(N / tall, 1), "unit": "matches/s",
+                                   "cores": threads, "seconds_per_pair": round(tall, 4),
+                                   "runs_s": [round(t, 4) for t in tsall],
+                                   "note": "OpenMP over queries and curvature rows; serial "
+                                           "tree build"},
             "host": host,
             "sample": (f"the full K3 pair 0 ({N} queries vs {N} targets), median of {reps} after "
                        "1 warm-up: extract_feature on both clouds + buildKDTree + "
@@ -207,7 +212,7 @@ def cpu_baseline_k2(src, tgt, reps):
     buildKDTree over the target row's features and nearestNeighborSearch for
     each source feature (oracle/_ref = utils/kdtree.c compiled as-is), which
     is what src/slam.c:162-172,230-244 runs per frame. 1 core (as the
-    reference) and all cores (OpenMP over rows); median of `reps` after one
+    reference) and N threads (OpenMP over rows, N = OMP_NUM_THREADS); median of `reps` after one
     warm-up."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     from pyoracle import Oracle
@@ -232,10 +237,11 @@ def cpu_baseline_k2(src, tgt, reps):
     tall, tsall = median_after_warmup(run(threads), reps)
     return {"value": round(nq[0] / t1, 1), "unit": "matches/s", "cores": 1, "kind": "reference",
             "seconds_per_pair": round(t1, 5), "runs_s": [round(t, 5) for t in ts1],
-            "all_cores": {"value": round(nq[0] / tall, 1), "unit": "matches/s",
-                          "cores": threads, "seconds_per_pair": round(tall, 5),
-                          "runs_s": [round(t, 5) for t in tsall],
-                          "note": "OpenMP over rows (build + queries) and curvature rows"},
+            f"threads_{threads}": {"value": round(nq[0] / tall, 1), "unit": "matches/s",
+                                   "cores": threads, "seconds_per_pair": round(tall, 5),
+                                   "runs_s": [round(t, 5) for t in tsall],
+                                   "note": "OpenMP over rows (build + queries) and curvature "
+                                           "rows"},
             "host": host_info(),
             "sample": (f"one {src.shape[0]}x{src.shape[1]} L9-shaped pair ({nq[0]} source-feature "
                        f"queries), median of {reps} after 1 warm-up: extract_feature x2 + per-row "
@@ -500,7 +506,7 @@ def main():
         pairs = hi - lo
         srcs, tgts = [], []
         for p in range(lo, hi):
-            s_h, t_h = synth.l9_pair(R, Cc, seed=p + 5)
+            s_h, t_h = synth.l9_pair(R, Cc, seed=p + 5, integer_mm=a.integer_mm)
             srcs.append(torch.from_numpy(s_h).to(dev))
             tgts.append(torch.from_numpy(t_h).to(dev))
             if a.workload == "k4" and p - lo >= 7:   # 8 distinct pairs, cycled
@@ -555,9 +561,11 @@ def main():
                     "reference KD semantics; its tree built only for rows with a distance tie)"
                     + (", RCCL all-gather of the match sets (idx + dist, 12 B per cell)"
                        if gather_buf is not None else ""))
-        data = "synthetic L9-shaped range images (navslam.synth.l9_pair), fixed seeds"
+        data = ("synthetic L9-shaped range images (navslam.synth.l9_pair), fixed seeds"
+                + (", coordinates rounded to whole mm" if a.integer_mm else ""))
         cfg_extra = {"points_per_cloud": N, "k": 1, "pairs_per_gpu": pairs, "mode": "rows",
-                     "tie_rows": tie_rows, "rows_per_step": pairs * R}
+                     "integer_mm": bool(a.integer_mm), "tie_rows": tie_rows,
+                     "rows_per_step": pairs * R}
 
     # warmup (grows the workspace, JITs nothing)
     for _ in range(a.warmup):

@@ -58,18 +58,24 @@ struct __align__(16) PRec {
 };
 
 // ---- k_knn tile geometry (LDS budget: 4 blocks of 192 threads per CU)
-constexpr int kTileThreads = 192;  // 3 waves: a ~145-query tile fills them
+#ifndef NAVGPU_KNN_TILE_THREADS
+#define NAVGPU_KNN_TILE_THREADS 192
+#define NAVGPU_KNN_TILE_REC 1568
+#define NAVGPU_KNN_TILE_COLS 136
+#define NAVGPU_KNN_TILE_Q 150.0
+#endif
+constexpr int kTileThreads = NAVGPU_KNN_TILE_THREADS;  // 3 waves: a ~145-query tile fills them
 // waves per SIMD k_knn's registers must allow: 5 blocks of 3 waves per CU
 // (the LDS limit) need 4, i.e. <= 128 VGPRs
 #ifndef NAVGPU_KNN_MINW
 #define NAVGPU_KNN_MINW 4
 #endif
 constexpr int kKnnMinWaves = NAVGPU_KNN_MINW;
-constexpr int kTileRec = 1568;     // staged records per tile (16 B each)
+constexpr int kTileRec = NAVGPU_KNN_TILE_REC;     // staged records per tile (16 B each)
 constexpr int kTilePairs = kTileRec / 2 + 2;  // two spare pairs: read-ahead
 constexpr int kZgOff = 4 * kTilePairs;        // floats from the XY plane to the ZG plane
-constexpr int kTileCols = 136;     // staged columns per tile + 1
-constexpr double kTileQueries = 150.0;  // target queries per tile
+constexpr int kTileCols = NAVGPU_KNN_TILE_COLS;     // staged columns per tile + 1
+constexpr double kTileQueries = NAVGPU_KNN_TILE_Q;  // target queries per tile
 // survivor lists (NAVGPU_KNN_LIST=1): keys below a threshold are appended to
 // a per-lane LDS list and inserted into the sorted K+1 in batches; off by
 // default (the list's LDS costs a block per CU, r3 A/B in DESIGN.md §4)
