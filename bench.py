@@ -83,7 +83,7 @@ def parse():
     p.add_argument("--traffic-csv", default=None,
                    help="comma-separated rocprofv3 --pmc counter_collection.csv files "
                         "(FETCH_SIZE and WRITE_SIZE passes) to derive HBM bytes")
-    p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_k3.json"),
+    p.add_argument("--traffic-json", default=None,
                    help="per-step HBM bytes measured by scripts/round_profile.sh (PMC passes)")
     p.add_argument("--no-traffic-json", action="store_true")
     p.add_argument("--no-stream-copy", action="store_true",
@@ -332,9 +332,11 @@ def run_k5(a, ws, rank, dev):
     qpf = (state["q"] - q0) / max(a.steps, 1)
     bytes_pf = int(24 * qpf + (24 + 24 + 12) * qpf)
     ach = bytes_pf / (gpu_us * 1e-6) / 1e9 if gpu_us > 0 else None
+    tj = load_traffic(a, {"workload": traffic_tag(a), "points_per_cloud": R * Cc})
     roof = {"bound": "hbm", "achieved": round(ach, 2) if ach else None, "peak": HBM_PEAK_GBS,
             "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 6) if ach else None,
-            "traffic": None, "kernel": "k_rows_build + k_rows_query (+ k_rows_corr) per frame",
+            "traffic": tj and tj.get("bytes_per_step"),
+            "kernel": "k_rows_build + k_rows_query (+ k_rows_corr) per frame",
             "avg_us": round(gpu_us, 2), "bytes_per_launch": bytes_pf,
             "bytes_model": "24 B/target feature (build) + 24 Q + 24 T + 12 Q (query), SURVEY 8d",
             "note": ("latency-bound per-row kernels; " + ("a frame is host-bound (sequential "
@@ -672,10 +674,9 @@ def main():
             if a.traffic_csv:
                 traffic = traffic_from_csv(a.traffic_csv.split(","))
                 build_traffic = traffic_from_csv(a.traffic_csv.split(","), BUILD_KERNELS)
-            elif not a.no_traffic_json and os.path.exists(a.traffic_json):
-                with open(a.traffic_json) as f:
-                    tj = json.load(f)
-                if tj.get("k") == a.k and tj.get("points_per_cloud") == N:
+            else:
+                tj = load_traffic(a, {"k": a.k, "points_per_cloud": N})
+                if tj is not None:
                     traffic = tj.get("bytes_per_step")
                     build_traffic = tj.get("build_bytes_per_step")
             roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
@@ -713,8 +714,11 @@ def main():
                     "note": "latency/LDS-bound per-row kernel; bytes model in DESIGN.md"}
         if a.workload != "k3" and dom_bytes and dom_n > 0:
             ach = dom_bytes / (dom_avg_us * 1e-6) / 1e9
+            tj = load_traffic(a, {"workload": traffic_tag(a), "pairs_per_step": pairs,
+                                  "points_per_cloud": N})
             roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
-                    "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 5), "traffic": None,
+                    "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 5),
+                    "traffic": tj and tj.get("bytes_per_step"),
                     "kernel": ("rows_match: k_curvature (both clouds) + k_rows_screen (exact "
                                "f64 argmin + runner-up per query) + the tree pass over tied "
                                "rows only"),
@@ -781,15 +785,44 @@ def main():
 QUERY_KERNELS = ("k_knn<", "k_knn_slow<")
 BUILD_KERNELS = ("k_bbox_partial", "k_grid_params", "k_bin_hist", "k_scan_sums",
                  "k_scan_apply", "k_bin_scatter", "k_bin_fine")
+# per-row workloads: the kernels of one step and the kernel launched once per
+# step (the per-step divisor)
+ROWS_KERNELS = ("k_curvature", "k_rows_screen", "k_rows_match")
+K5_KERNELS = ("k_rows_build", "k_rows_query", "k_rows_corr")
+TRAFFIC_SETS = {"k3": (QUERY_KERNELS, "k_knn<"), "k3_build": (BUILD_KERNELS, "k_knn<"),
+                "rows": (ROWS_KERNELS, "k_rows_screen"), "k5": (K5_KERNELS, "k_rows_build")}
 
 
-def pmc_bytes(paths, kernel_subs):
-    """HBM bytes per K3 step of the kernels whose name contains one of
+def traffic_tag(a):
+    """profiles/traffic_<tag>.json: the PMC bytes a bench line of this
+    workload quotes (k3, k2, k2i, k4, k4i, k5, k5f)."""
+    t = a.workload
+    if a.workload in ("k2", "k4") and a.integer_mm:
+        t += "i"
+    if a.workload == "k5" and a.k5_mode == "fast":
+        t += "f"
+    return t
+
+
+def load_traffic(a, match):
+    """The traffic json of this workload if its signature matches `match`."""
+    if a.no_traffic_json:
+        return None
+    path = a.traffic_json or os.path.join(ROOT, "profiles", f"traffic_{traffic_tag(a)}.json")
+    if not os.path.exists(path):
+        return None
+    with open(path) as f:
+        tj = json.load(f)
+    return tj if all(tj.get(k) == v for k, v in match.items()) else None
+
+
+def pmc_bytes(paths, kernel_subs, anchor="k_knn<"):
+    """HBM bytes per step of the kernels whose name contains one of
     `kernel_subs`, from rocprofv3 --pmc counter CSVs (FETCH_SIZE in one pass,
     WRITE_SIZE in another; both in KB). Per step = total / launches of the
-    query kernel k_knn<K> (one per step). Returns {"fetch_raw", "write",
-    "bytes"}: FETCH_SIZE as counted, WRITE_SIZE, and FETCH_SIZE x 2 (the
-    gfx950 correction, MI355X_MICROARCH.md HBM section) + WRITE_SIZE."""
+    `anchor` kernel (one per step). Returns {"fetch_raw", "write", "bytes"}:
+    FETCH_SIZE as counted, WRITE_SIZE, and FETCH_SIZE x 2 (the gfx950
+    correction, MI355X_MICROARCH.md HBM section) + WRITE_SIZE."""
     import csv
     fetch, write = 0.0, 0.0
     launches = {}
@@ -798,7 +831,7 @@ def pmc_bytes(paths, kernel_subs):
             for r in csv.DictReader(f):
                 name = r.get("Kernel_Name", "")
                 c = r.get("Counter_Name")
-                if "k_knn<" in name:
+                if anchor in name:
                     launches.setdefault(c, set()).add(r.get("Dispatch_Id"))
                 if not any(k in name for k in kernel_subs):
                     continue

@@ -34,6 +34,14 @@ __global__ __launch_bounds__(256) void k_op(uint32_t *out, int iters, uint32_t s
       if (OP == 13) asm volatile("v_med3_f32 %0, %0, %1, %2" : "+v"(fa[j].x) : "v"(fb.x), "v"(fc.x));
       if (OP == 14) asm volatile("v_pk_max_u16 %0, %0, %1" : "+v"(a[j]) : "v"(b));
       if (OP == 15) asm volatile("v_sub_f32_e32 %0, %1, %0" : "+v"(fa[j].x) : "v"(fb.x));
+      if (OP == 16) asm volatile("v_min_f32_e32 %0, %1, %0" : "+v"(fa[j].x) : "v"(fb.x));
+      if (OP == 17) asm volatile("v_max_f32_e32 %0, %1, %0" : "+v"(fa[j].x) : "v"(fb.x));
+      if (OP == 18) asm volatile("v_min3_f32 %0, %0, %1, %2" : "+v"(fa[j].x) : "v"(fb.x), "v"(fc.x));
+      if (OP == 19) asm volatile("v_perm_b32 %0, %0, %1, %2" : "+v"(a[j]) : "v"(b), "v"(c));
+      if (OP == 20) asm volatile("v_cndmask_b32_e32 %0, %1, %0, vcc" : "+v"(a[j]) : "v"(b));
+      if (OP == 21) asm volatile("v_med3_i32 %0, %0, %1, %2" : "+v"(a[j]) : "v"(b), "v"(c));
+      if (OP == 22) asm volatile("v_lshl_or_b32 %0, %0, 8, %1" : "+v"(a[j]) : "v"(b));
+      if (OP == 23) asm volatile("v_max_f32_e64 %0, %1, %0" : "+v"(fa[j].x) : "v"(fb.x));
     }
   }
   uint32_t acc = 0;
@@ -69,13 +77,17 @@ int main() {
   const char *names[] = {"v_add_u32_e32", "v_min_u32_e32", "v_med3_u32", "v_min3_u32", "v_add_f32_e32",
                          "v_fma_f32", "v_pk_fma_f32", "v_pk_add_f32", "v_and_or_b32", "v_xor_b32_e32",
                          "v_max_u32_e32", "v_mul_f32_e32", "v_pk_mul_f32", "v_med3_f32", "v_pk_max_u16",
-                         "v_sub_f32_e32"};
+                         "v_sub_f32_e32", "v_min_f32_e32", "v_max_f32_e32", "v_min3_f32",
+                         "v_perm_b32", "v_cndmask_b32", "v_med3_i32", "v_lshl_or_b32",
+                         "v_max_f32_e64"};
   // waves per SIMD: 256 CUs x 4 SIMDs; a 256-thread block = one wave per SIMD
-  for (int wps : {1, 2, 4, 8}) {
+  for (int wps : {4, 8}) {
     const int blocks = 256 * wps;
-    float (*fns[16])(uint32_t *, int, int) = {run<0>, run<1>, run<2>, run<3>, run<4>, run<5>, run<6>, run<7>,
-                                              run<8>, run<9>, run<10>, run<11>, run<12>, run<13>, run<14>, run<15>};
-    for (int op = 0; op < 16; ++op) {
+    float (*fns[24])(uint32_t *, int, int) = {
+        run<0>,  run<1>,  run<2>,  run<3>,  run<4>,  run<5>,  run<6>,  run<7>,
+        run<8>,  run<9>,  run<10>, run<11>, run<12>, run<13>, run<14>, run<15>,
+        run<16>, run<17>, run<18>, run<19>, run<20>, run<21>, run<22>, run<23>};
+    for (int op = 0; op < 24; ++op) {
       const float ms = fns[op](d, blocks, iters);
       const double wave_ops_per_simd = (double)wps * iters * NC;
       printf("wps=%d %-15s %.2f cycles/op/SIMD (clock attr %.2f GHz)\n", wps, names[op],

@@ -1,13 +1,14 @@
 #!/bin/bash
 # Round evidence in one gpurun session (outputs under gpurun_out/<tag>/):
-#   GPU tests -> smoke -> K3 kernel trace -> FETCH_SIZE / WRITE_SIZE passes
-#   (separate --pmc runs, no trace domains) -> traffic json -> K3 bench line
-#   (traffic + CPU baseline) -> K2, K4, K5 (exact, fast) bench lines.
-# A crash/abort/timeout ends the script.
-TAG=${1:-r1}
+#   GPU tests -> smoke -> K3 kernel trace -> per workload (K3, K2, K2 integer-mm,
+#   K4, K4 integer-mm, K5 fast) a FETCH_SIZE and a WRITE_SIZE pass (separate
+#   --pmc runs, no trace domains) -> traffic_<w>.json -> the bench lines, each
+#   quoting its own traffic json (K3 also with the CPU baseline).
+# A crash/abort/timeout ends the script. SKIP_TESTS=1 skips pytest + smoke.
+TAG=${1:-r3}
 OUT=gpurun_out/$TAG
 mkdir -p "$OUT"
-export NAVSLAM_QUIET=1
+export NAVSLAM_QUIET=1 PYTHONUNBUFFERED=1
 fatal() { [ "$1" -ge 124 ] || [ "$1" -eq 134 ] || [ "$1" -eq 139 ]; }
 step() {  # step <name> <timeout> cmd...
   local name=$1 tmo=$2; shift 2
@@ -15,24 +16,41 @@ step() {  # step <name> <timeout> cmd...
   timeout -k 10 "$tmo" "$@" > "$OUT/$name.log" 2>&1
   local rc=$?
   echo "== $name rc=$rc" | tee -a "$OUT/steps.log"
-  tail -n 2 "$OUT/$name.log"
+  tail -n 2 "$OUT/$name.log" | cut -c1-300
   if fatal $rc; then echo "FATAL in $name, stopping"; exit $rc; fi
   return 0
 }
-step pytest 900 python3 -u -m pytest tests -m gpu -v -x --timeout 240 --timeout-method=thread
-step smoke 300 python3 -c "import __graft_entry__ as g; g.smoke()"
+if [ -z "$SKIP_TESTS" ]; then
+  step pytest 900 python3 -u -m pytest tests -m gpu -v -x --timeout 240 --timeout-method=thread
+  step smoke 300 python3 -c "import __graft_entry__ as g; g.smoke()"
+fi
 export TMPDIR=/tmp
-BENCH="bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-traffic-json"
-step trace 600 rocprofv3 --kernel-trace --stats -d "$OUT/trace" -o run --output-format csv -- python3 $BENCH --json-out "$OUT/bench_traced.json"
-step pmc_fetch 300 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc_fetch" -o run --output-format csv -- python3 $BENCH
-step pmc_write 300 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmc_write" -o run --output-format csv -- python3 $BENCH
-F=$(find "$OUT/pmc_fetch" -name "*counter_collection.csv" | head -1)
-W=$(find "$OUT/pmc_write" -name "*counter_collection.csv" | head -1)
-step traffic 120 python3 scripts/traffic_json.py "$F" "$W" "$OUT/traffic_k3.json" "$TAG"
-step bench 600 python3 bench.py --traffic-json "$OUT/traffic_k3.json" --json-out "$OUT/bench_k3.json"
-step bench_k2 300 python3 bench.py --workload k2 --steps 10 --json-out "$OUT/bench_k2.json"
-step bench_k4 400 python3 bench.py --workload k4 --steps 3 --warmup 1 --json-out "$OUT/bench_k4.json"
+Q="--no-cpu-baseline --no-traffic-json --no-stream-copy"
+step trace_k3 600 rocprofv3 --kernel-trace --stats -d "$OUT/trace_k3" -o run --output-format csv -- python3 bench.py --steps 20 --warmup 3 $Q --json-out "$OUT/bench_k3_traced.json"
+pmc() {  # pmc <w> <traffic args> -- <bench args>
+  local w=$1; shift
+  local targs=()
+  while [ "$1" != "--" ]; do targs+=("$1"); shift; done; shift
+  step pmc_fetch_$w 300 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc_fetch_$w" -o run --output-format csv -- python3 bench.py "$@" $Q
+  step pmc_write_$w 300 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmc_write_$w" -o run --output-format csv -- python3 bench.py "$@" $Q
+  local F W
+  F=$(find "$OUT/pmc_fetch_$w" -name "*counter_collection.csv" | head -1)
+  W=$(find "$OUT/pmc_write_$w" -name "*counter_collection.csv" | head -1)
+  step traffic_$w 120 python3 scripts/traffic_json.py "$F" "$W" "$OUT/traffic_$w.json" "$TAG" --workload "$w" "${targs[@]}" --src "python3 bench.py $*"
+}
+pmc k3 -- --steps 20 --warmup 3
+pmc k2 --points 262144 --pairs 1 -- --workload k2 --steps 10
+pmc k2i --points 262144 --pairs 1 -- --workload k2 --integer-mm --steps 10
+pmc k4 --points 262144 --pairs 256 -- --workload k4 --steps 2 --warmup 1
+pmc k4i --points 262144 --pairs 256 -- --workload k4 --integer-mm --steps 2 --warmup 1
+pmc k5f --points 262144 -- --workload k5 --k5-mode fast --steps 20 --warmup 2
+step bench_k3 600 python3 bench.py --traffic-json "$OUT/traffic_k3.json" --json-out "$OUT/bench_k3.json"
+step bench_k3_inflight1 300 python3 bench.py --inflight 1 --no-cpu-baseline --traffic-json "$OUT/traffic_k3.json" --json-out "$OUT/bench_k3_inflight1.json"
+step bench_k2 300 python3 bench.py --workload k2 --steps 10 --traffic-json "$OUT/traffic_k2.json" --json-out "$OUT/bench_k2.json"
+step bench_k2i 300 python3 bench.py --workload k2 --integer-mm --steps 10 --traffic-json "$OUT/traffic_k2i.json" --json-out "$OUT/bench_k2i.json"
+step bench_k4 400 python3 bench.py --workload k4 --steps 3 --warmup 1 --traffic-json "$OUT/traffic_k4.json" --json-out "$OUT/bench_k4.json"
+step bench_k4i 400 python3 bench.py --workload k4 --integer-mm --steps 3 --warmup 1 --no-cpu-baseline --traffic-json "$OUT/traffic_k4i.json" --json-out "$OUT/bench_k4i.json"
 step bench_k5 400 python3 bench.py --workload k5 --steps 30 --warmup 2 --json-out "$OUT/bench_k5.json"
-step bench_k5_fast 400 python3 bench.py --workload k5 --k5-mode fast --steps 30 --warmup 2 --json-out "$OUT/bench_k5_fast.json"
-step trace_k5 400 rocprofv3 --kernel-trace --stats -d "$OUT/trace_k5" -o run --output-format csv -- python3 bench.py --workload k5 --k5-mode fast --steps 20 --warmup 2 --no-cpu-baseline
+step bench_k5_fast 400 python3 bench.py --workload k5 --k5-mode fast --steps 30 --warmup 2 --traffic-json "$OUT/traffic_k5f.json" --json-out "$OUT/bench_k5_fast.json"
+step trace_k5 400 rocprofv3 --kernel-trace --stats -d "$OUT/trace_k5" -o run --output-format csv -- python3 bench.py --workload k5 --k5-mode fast --steps 20 --warmup 2 --no-cpu-baseline --no-traffic-json
 echo done
