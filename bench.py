@@ -698,8 +698,8 @@ def main():
             # and its measured traffic
             b_ms, b_n = kt.get("knn_build", (0.0, 0))
             if b_n:
-                bld = {"kernels": ("k_bbox_partial + k_grid_params + k_bin_hist + k_scan_sums + "
-                                   "k_scan_apply + k_bin_scatter + k_bin_fine (both clouds binned)"),
+                bld = {"kernels": ("k_bbox_partial + k_grid_params + k_bin_hist + k_bin_colscan + "
+                                   "k_bin_scatter + k_bin_fine (both clouds binned)"),
                        "avg_us": round(1000.0 * b_ms / b_n, 2),
                        "bytes_model": "24 B/target read (SURVEY 8d); the query binning is extra",
                        "algorithmic_bytes": 24 * N, "traffic": build_traffic}
@@ -783,8 +783,8 @@ def main():
 
 
 QUERY_KERNELS = ("k_knn<", "k_knn_slow<")
-BUILD_KERNELS = ("k_bbox_partial", "k_grid_params", "k_bin_hist", "k_scan_sums",
-                 "k_scan_apply", "k_bin_scatter", "k_bin_fine")
+BUILD_KERNELS = ("k_bbox_partial", "k_grid_params", "k_bin_hist", "k_bin_colscan",
+                 "k_bin_scatter", "k_bin_fine")
 # per-row workloads: the kernels of one step and the kernel launched once per
 # step (the per-step divisor)
 ROWS_KERNELS = ("k_curvature", "k_rows_screen", "k_rows_match")

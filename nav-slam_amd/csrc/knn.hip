@@ -12,7 +12,7 @@
 // of each kernel):
 //   k_bbox_partial, k_grid_params   target bbox -> uniform grid (cells of
 //                                   h/sx x h x h, ~occ targets per h^3)
-//   k_bin_hist, k_scan_*, k_bin_scatter, k_bin_fine
+//   k_bin_hist, k_bin_colscan, k_bin_scatter, k_bin_fine
 //                                   both clouds counting-sorted by cell
 //                                   (LDS atomics only): the targets as
 //                                   cell-sorted 32-B records (f64 point,
@@ -259,55 +259,69 @@ __device__ __forceinline__ int cell_of(const double *p, const GridParams &G) {
          cell_axis(p[0], G, 0);
 }
 
-constexpr int kScanBlock = 1024, kScanPer = 4, kScanTile = kScanBlock * kScanPer;
+constexpr int kBinMaxBuckets = 4096;  // coarse buckets per side (k_bin_*)
 
-__global__ __launch_bounds__(kScanBlock) void k_scan_sums(const int *__restrict__ in, int n,
-                                                          int *__restrict__ bsum) {
-  __shared__ int scratch[40];
-  const int base = blockIdx.x * kScanTile + threadIdx.x * kScanPer;
-  int s = 0;
+// ---- (bucket, block) offsets of the binning (k_bin_*) ---------------------
+// The count table is block-major per side, T[tab + blk * nb + b], so that
+// k_bin_hist writes and k_bin_scatter reads one contiguous row per block.
+// k_bin_colscan turns each bucket's column into an exclusive prefix over the
+// blocks, in place, and its total into btot[side * nb + b]; the bucket bases
+// (the exclusive scan of btot) are recomputed in LDS by every k_bin_scatter
+// block (cheaper than a one-block launch); block 0 of each side publishes them
+// to bbase[side * (nb + 1) + 0 .. nb] for k_bin_fine.
+constexpr int kColB = 64;              // buckets per k_bin_colscan block
+constexpr int kColY = 16;              // block-row chunks per bucket column
+__global__ __launch_bounds__(kColB * kColY) void k_bin_colscan(int *__restrict__ T, int nb,
+                                                               int tab0, int nblk0, int tab1,
+                                                               int nblk1, int *__restrict__ btot) {
+  __shared__ int part[kColY][kColB];
+  const int per_side = (nb + kColB - 1) / kColB;
+  const int side = (int)blockIdx.x >= per_side ? 1 : 0;
+  const int b = ((int)blockIdx.x - side * per_side) * kColB + (int)threadIdx.x % kColB;
+  const int y = (int)threadIdx.x / kColB;
+  const int tab = side ? tab1 : tab0, nblk = side ? nblk1 : nblk0;
+  const int ch = (nblk + kColY - 1) / kColY;
+  const int k0 = min(nblk, y * ch), k1 = min(nblk, k0 + ch);
+  // a chunk's counts: every load in flight before any is used
+  constexpr int U = 16;
+  int v[U], sum = 0;
+  for (int k = k0; k < k1; k += U) {
 #pragma unroll
-  for (int k = 0; k < kScanPer; ++k)
-    if (base + k < n) s += in[base + k];
-  int total;
-  block_excl_scan(s, scratch, &total);
-  if (threadIdx.x == 0) bsum[blockIdx.x] = total;
-}
-
-__global__ __launch_bounds__(kScanBlock) void k_scan_apply(const int *__restrict__ in, int n,
-                                                           const int *__restrict__ bsum,
-                                                           int *__restrict__ out) {
-  __shared__ int scratch[40];
-  const int base = blockIdx.x * kScanTile + threadIdx.x * kScanPer;
-  int v[kScanPer];
-  int s = 0;
+    for (int u = 0; u < U; ++u) v[u] = (b < nb && k + u < k1) ? T[tab + (k + u) * nb + b] : 0;
 #pragma unroll
-  for (int k = 0; k < kScanPer; ++k) {
-    v[k] = base + k < n ? in[base + k] : 0;
-    s += v[k];
+    for (int u = 0; u < U; ++u) sum += v[u];
   }
-  // this block's offset: the sum of the block totals before it, read straight
-  // from bsum (a separate top-level scan launch costs more than these reads)
-  int pre = 0;
-  for (int i = threadIdx.x; i < (int)blockIdx.x; i += blockDim.x) pre += bsum[i];
-  int total, ptot;
-  block_excl_scan(pre, scratch, &ptot);
-  __syncthreads();  // scratch is reused by the next scan
-  int off = block_excl_scan(s, scratch, &total) + ptot;
+  part[y][threadIdx.x % kColB] = sum;
+  __syncthreads();
+  int pre = 0, tot = 0;
 #pragma unroll
-  for (int k = 0; k < kScanPer; ++k) {
-    if (base + k < n) out[base + k] = off;
-    off += v[k];
+  for (int w = 0; w < kColY; ++w) {
+    const int c = part[w][threadIdx.x % kColB];
+    pre += w < y ? c : 0;
+    tot += c;
   }
+  if (b >= nb) return;
+  for (int k = k0; k < k1; k += U) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) v[u] = k + u < k1 ? T[tab + (k + u) * nb + b] : 0;
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (k + u < k1) {
+        T[tab + (k + u) * nb + b] = pre;
+        pre += v[u];
+      }
+  }
+  if (y == 0) btot[side * nb + b] = tot;
 }
 
 // ---- cell binning: counting sort of both clouds by grid cell --------------
 // Scattered global atomics run at the memory side on this part (~24 G/s
 // whatever their scope), so the sort uses none: LDS histograms and LDS ranks.
 //  k_bin_hist    each block takes a contiguous chunk of points and counts
-//                their coarse bucket (cell >> shift) in LDS; counts land in a
-//                bucket-major table[b * nblk + block], so ONE exclusive scan
-//                of the table gives every (bucket, block) its output offset.
+//                their coarse bucket (cell >> shift) in LDS; the counts land
+//                in a block-major table[block * nb + b] (one contiguous row
+//                per block); k_bin_colscan turns it into every (bucket,
+//                block)'s offset within its bucket and the buckets' totals.
 //  k_bin_scatter same chunks: each point gets an LDS rank within its
 //                (bucket, block) and moves to the coarse-bucketed array
 //                (BinPt, 32 B).
@@ -329,7 +343,6 @@ struct BinSide {
   const double *p;
   int n, P, nblk;
   int tab;  // offset of this side's table in the concatenated table
-  int sub;  // subtracted from scanned offsets (targets' total, for side 1)
   int *start;
   BinPt *bin;    // coarse-bucketed points
   PRec *sorted;  // targets: cell-sorted records
@@ -339,7 +352,6 @@ struct BinJob {
   BinSide s[2];
   int shift, nb;  // buckets per side
 };
-constexpr int kBinMaxBuckets = 4096;
 constexpr int kBinMaxShift = 15;
 constexpr int kBinUnroll = 8;  // points per thread with loads in flight
 constexpr int kBinP = 4096;    // minimum points per k_bin_hist / k_bin_scatter block
@@ -388,18 +400,38 @@ __global__ __launch_bounds__(256) void k_bin_hist(BinJob J, const GridParams *__
   __syncthreads();
   bin_chunk(S, blk, G, [&](int, const P3 &, int c) { atomicAdd(&hist[c >> J.shift], 1); });
   __syncthreads();
-  for (int b = threadIdx.x; b < J.nb; b += blockDim.x) table[S.tab + b * S.nblk + blk] = hist[b];
-  if (blk == 0 && threadIdx.x == 0) table[S.tab + J.nb * S.nblk] = 0;  // sentinel
+  for (int b = threadIdx.x; b < J.nb; b += blockDim.x) table[S.tab + blk * J.nb + b] = hist[b];
 }
 
 __global__ __launch_bounds__(256) void k_bin_scatter(BinJob J, const GridParams *__restrict__ gp,
-                                                     const int *__restrict__ offs) {
+                                                     const int *__restrict__ offs,
+                                                     const int *__restrict__ btot,
+                                                     int *__restrict__ bbase) {
   __shared__ int cur[kBinMaxBuckets];
+  __shared__ int scratch[40];
   int blk = blockIdx.x;
-  const BinSide S = J.s[bin_side(J, blk)];
+  const int side = bin_side(J, blk);
+  const BinSide S = J.s[side];
   const GridParams G = *gp;
-  for (int b = threadIdx.x; b < J.nb; b += blockDim.x)
-    cur[b] = offs[S.tab + b * S.nblk + blk] - S.sub;
+  // the side's bucket bases: exclusive scan of btot, each thread a run
+  {
+    const int *bt = btot + side * J.nb;
+    const int per = (J.nb + blockDim.x - 1) / blockDim.x;
+    const int j0 = min(J.nb, (int)threadIdx.x * per), j1 = min(J.nb, j0 + per);
+    int sum = 0;
+    for (int j = j0; j < j1; ++j) sum += bt[j];
+    int total;
+    int acc = block_excl_scan(sum, scratch, &total);
+    // the side's first block also publishes the bases for k_bin_fine
+    int *bo = blk == 0 ? bbase + side * (J.nb + 1) : nullptr;
+    for (int j = j0; j < j1; ++j) {
+      const int v = bt[j];
+      cur[j] = acc + offs[S.tab + blk * J.nb + j];
+      if (bo) bo[j] = acc;
+      acc += v;
+    }
+    if (bo && threadIdx.x == 0) bo[J.nb] = total;
+  }
   __syncthreads();
   bin_chunk(S, blk, G, [&](int i, const P3 &v, int c) {
     const int pos = atomicAdd(&cur[c >> J.shift], 1);
@@ -420,7 +452,7 @@ __global__ __launch_bounds__(256) void k_bin_scatter(BinJob J, const GridParams 
 // rest.
 __global__ __launch_bounds__(kBinFineThreads) void k_bin_fine(BinJob J,
                                                               const GridParams *__restrict__ gp,
-                                                              const int *__restrict__ offs,
+                                                              const int *__restrict__ bbase,
                                                               int nscan) {
   extern __shared__ int cnt[];  // 2^shift
   __shared__ int scratch[40];
@@ -428,8 +460,7 @@ __global__ __launch_bounds__(kBinFineThreads) void k_bin_fine(BinJob J,
   const int b = blockIdx.x - (side ? J.nb : 0);
   const BinSide S = J.s[side];
   const int ncell = 1 << J.shift, base = b << J.shift;
-  const int lo = offs[S.tab + b * S.nblk] - S.sub;
-  const int hi = offs[S.tab + (b + 1) * S.nblk] - S.sub;
+  const int lo = bbase[side * (J.nb + 1) + b], hi = bbase[side * (J.nb + 1) + b + 1];
   const BinPt *src = S.bin;
   for (int j = threadIdx.x; j < ncell; j += blockDim.x) cnt[j] = 0;
   __syncthreads();
@@ -1336,28 +1367,27 @@ static int knn_run(navgpu_ctx *ctx, const double *tgt, size_t nt, const double *
     S.P = (int)std::max<size_t>(kBinP, (ns[side] / 2000 + 256) / 256 * 256);
     S.nblk = (int)std::max<size_t>(1, (ns[side] + S.P - 1) / S.P);
     S.tab = (int)ntab;
-    S.sub = side ? (int)nt : 0;
-    ntab += (long long)J.nb * S.nblk + 1;
+    ntab += (long long)J.nb * S.nblk;
   }
-  const int nbs = (int)((ntab + kScanTile - 1) / kScanTile);
-  if (nbs > kScanTile) {
-    set_err("knn: binning table of %lld entries exceeds the scan capacity", ntab);
+  if (ntab >= INT32_MAX) {
+    set_err("knn: binning table of %lld entries exceeds the int range", ntab);
     return NAVGPU_ERANGE;
   }
   const int nparts = (int)std::min<size_t>(kBBoxBlocks, std::max<size_t>(1, grid1d(nt, 256)));
   double *part;
   GridParams *gp;
-  int *tab, *offs, *tstart, *qstart, *bsum, *counters;
+  int *tab, *tstart, *qstart, *bbase, *counters;
   BinPt *tbin = nullptr, *qbin;
   PRec *tsort = nullptr;
   int *qperm;
   RC(ws(ctx, kBBox, (size_t)kBBoxBlocks * 6, &part));
   RC(ws(ctx, kParams, 1, &gp));
   RC(ws(ctx, kCnt, (size_t)ntab, &tab));
-  RC(ws(ctx, kCellId, (size_t)ntab, &offs));
   RC(ws(ctx, kStart, nscan, &tstart));
   RC(ws(ctx, kQStart, nscan, &qstart));
-  RC(ws(ctx, kBSum, nbs, &bsum));
+  int *btot;
+  RC(ws(ctx, kBSum, 2 * (size_t)J.nb, &btot));
+  RC(ws(ctx, kCellId, 2 * ((size_t)J.nb + 1), &bbase));
   RC(ws(ctx, kStats, 4, &counters));  // zeroed by k_grid_params
   if (nt) {
     RC(ws(ctx, kSlotBuf, nt, &tbin));
@@ -1388,19 +1418,19 @@ static int knn_run(navgpu_ctx *ctx, const double *tgt, size_t nt, const double *
     const dim3 gb(J.s[0].nblk + J.s[1].nblk);
     hipLaunchKernelGGL(k_bin_hist, gb, dim3(256), 0, s, J, gp, tab);
     CHECK_LAUNCH("k_bin_hist");
-    const int ntabi = (int)ntab;
-    hipLaunchKernelGGL(k_scan_sums, dim3(nbs), dim3(kScanBlock), 0, s, tab, ntabi, bsum);
-    CHECK_LAUNCH("k_scan_sums");
-    hipLaunchKernelGGL(k_scan_apply, dim3(nbs), dim3(kScanBlock), 0, s, tab, ntabi, bsum, offs);
-    CHECK_LAUNCH("k_scan_apply");
-    hipLaunchKernelGGL(k_bin_scatter, gb, dim3(256), 0, s, J, gp, (const int *)offs);
+    const dim3 gc(2 * ((J.nb + kColB - 1) / kColB));
+    hipLaunchKernelGGL(k_bin_colscan, gc, dim3(kColB * kColY), 0, s, tab, J.nb, J.s[0].tab,
+                       J.s[0].nblk, J.s[1].tab, J.s[1].nblk, btot);
+    CHECK_LAUNCH("k_bin_colscan");
+    hipLaunchKernelGGL(k_bin_scatter, gb, dim3(256), 0, s, J, gp, (const int *)tab,
+                       (const int *)btot, bbase);
     CHECK_LAUNCH("k_bin_scatter");
     const size_t lds = (size_t)4 << shift;
     if (lds > 48 * 1024)
       HIP_TRY(hipFuncSetAttribute((const void *)k_bin_fine,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     hipLaunchKernelGGL(k_bin_fine, dim3(2 * J.nb), dim3(kBinFineThreads), lds, s, J, gp,
-                       (const int *)offs, nscan);
+                       (const int *)bbase, nscan);
     CHECK_LAUNCH("k_bin_fine");
   }
   KnnLists lists;
