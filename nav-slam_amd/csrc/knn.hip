@@ -347,8 +347,6 @@ struct BinSide {
   BinPt *bin;    // coarse-bucketed points
   PRec *sorted;  // targets: cell-sorted records
   int *perm;     // queries: cell-sorted position -> bucketed position
-  int *cellv;    // queries: the cell of each bucketed point (k_bin_fine reads
-                 // these 4 B instead of the 32-B record)
 };
 struct BinJob {
   BinSide s[2];
@@ -444,7 +442,6 @@ __global__ __launch_bounds__(256) void k_bin_scatter(BinJob J, const GridParams 
     t.idx = i;
     t.cell = c;
     S.bin[pos] = t;
-    if (S.cellv) S.cellv[pos] = c;
   });
 }
 
@@ -475,7 +472,7 @@ __global__ __launch_bounds__(kBinFineThreads) void k_bin_fine(BinJob J,
     const int i = lo + u * bd + (int)threadIdx.x;
     if (i < held_end) {
       if (side)
-        hold[u].cell = S.cellv[i];
+        hold[u].cell = src[i].cell;
       else
         hold[u] = src[i];
     }
@@ -485,8 +482,7 @@ __global__ __launch_bounds__(kBinFineThreads) void k_bin_fine(BinJob J,
     const int i = lo + u * bd + (int)threadIdx.x;
     if (i < held_end) atomicAdd(&cnt[hold[u].cell - base], 1);
   }
-  for (int i = held_end + (int)threadIdx.x; i < hi; i += bd)
-    atomicAdd(&cnt[(side ? S.cellv[i] : src[i].cell) - base], 1);
+  for (int i = held_end + (int)threadIdx.x; i < hi; i += bd) atomicAdd(&cnt[src[i].cell - base], 1);
   __syncthreads();
   // exclusive scan over the bucket's cells: each thread owns a contiguous run
   const int per = ncell / bd;  // ncell is a multiple of the block size
@@ -522,15 +518,7 @@ __global__ __launch_bounds__(kBinFineThreads) void k_bin_fine(BinJob J,
     const int i = lo + u * bd + (int)threadIdx.x;
     if (i < held_end) place(hold[u], i);
   }
-  for (int i = held_end + (int)threadIdx.x; i < hi; i += bd) {
-    if (side) {
-      BinPt e;
-      e.cell = S.cellv[i];
-      place(e, i);
-    } else {
-      place(src[i], i);
-    }
-  }
+  for (int i = held_end + (int)threadIdx.x; i < hi; i += bd) place(src[i], i);
 }
 
 // ============================================================ k-NN helpers
@@ -1417,8 +1405,6 @@ static int knn_run(navgpu_ctx *ctx, const double *tgt, size_t nt, const double *
   J.s[1].sorted = nullptr;
   J.s[0].perm = nullptr;
   J.s[1].perm = qperm;
-  J.s[0].cellv = nullptr;
-  RC(ws(ctx, kQSlot, nq, &J.s[1].cellv));
   hipStream_t s = ctx->stream;
   {
     TimedRegion tb(ctx, "knn_build");
