@@ -773,9 +773,17 @@ __global__ __launch_bounds__(kRowsBlock) void k_rows_match(
 // SoA features (24 C), FCOL/P/T (6 C) and the walk stacks (4 NT x 14).
 // Results are identical to k_rows_match.
 constexpr int kLeanMaxC = 2048;  // in-place permutation: <= kLeanMaxC / NT per thread
+// (r3) the SoA features are sized for F <= C of them: a tie pass runs first
+// at F = kLeanF (three rows per CU instead of two), then again at F = C for
+// the rows whose feature count exceeded it (the others return at once); tree
+// walks, only the tied queries' there, take one wave
+constexpr int kLeanF = 1536;
 
-__host__ __device__ inline int rows_lean_lds(int C, int nt) {
-  return align16(24 * C) + 3 * align16(2 * C) + align16(4 * nt * kStackDepth) + align16(4 * 40);
+__host__ __device__ inline int rows_lean_walkers(bool tie, int nt) { return tie ? kWave : nt; }
+
+__host__ __device__ inline int rows_lean_lds(int C, int F, int walkers) {
+  return align16(24 * F) + 3 * align16(2 * C) + align16(4 * walkers * kStackDepth) +
+         align16(4 * 40);
 }
 
 // src/slam.c:16-58 for column j of a row read from global memory
@@ -790,19 +798,20 @@ __global__ __launch_bounds__(NT) void k_rows_match_lean(
     const double *__restrict__ src, const double *__restrict__ tgt, int R,
     int C, int32_t *__restrict__ src_mask, int32_t *__restrict__ tgt_mask,
     int32_t *__restrict__ nn_idx, double *__restrict__ nn_dist,
-    const int32_t *__restrict__ tie, int S) {
+    const int32_t *__restrict__ tie, int S, int F, int done_le) {
   constexpr int kHold = kLeanMaxC / NT;
   const int r = blockIdx.x;
   if (tie && !row_has_tie(tie, r, S)) return;  // uniform
   const size_t rowoff = (size_t)r * C;
   const int pair_row0 = (r % R) * C;
-  double *FC = (double *)smem;
-  uint16_t *FCOL = (uint16_t *)(smem + align16(24 * C));
-  uint16_t *P = (uint16_t *)(smem + align16(24 * C) + align16(2 * C));
-  uint16_t *T = (uint16_t *)(smem + align16(24 * C) + 2 * align16(2 * C));
-  uint32_t *stk = (uint32_t *)(smem + align16(24 * C) + 3 * align16(2 * C));
-  int *scan = (int *)(smem + align16(24 * C) + 3 * align16(2 * C) +
-                      align16(4 * NT * kStackDepth));
+  const int walkers = rows_lean_walkers(tie != nullptr, NT);
+  double *FC = (double *)smem;  // SoA, stride F
+  uint16_t *FCOL = (uint16_t *)(smem + align16(24 * F));
+  uint16_t *P = (uint16_t *)(smem + align16(24 * F) + align16(2 * C));
+  uint16_t *T = (uint16_t *)(smem + align16(24 * F) + 2 * align16(2 * C));
+  uint32_t *stk = (uint32_t *)(smem + align16(24 * F) + 3 * align16(2 * C));
+  int *scan = (int *)(smem + align16(24 * F) + 3 * align16(2 * C) +
+                      align16(4 * walkers * kStackDepth));
   // target row: features (flag in T), compacted SoA in column order
   const double *tg = tgt + 3 * rowoff;
   for (int j = threadIdx.x; j < C; j += NT) {
@@ -814,12 +823,17 @@ __global__ __launch_bounds__(NT) void k_rows_match_lean(
   const int n = block_compact(
       C, scan, [&](int j) { return T[j] != 0; },
       [&](int j, int pos) {
-        FC[pos] = tg[3 * j];
-        FC[C + pos] = tg[3 * j + 1];
-        FC[2 * C + pos] = tg[3 * j + 2];
-        FCOL[pos] = (uint16_t)j;
+        if (pos < F) {
+          FC[pos] = tg[3 * j];
+          FC[F + pos] = tg[3 * j + 1];
+          FC[2 * F + pos] = tg[3 * j + 2];
+          FCOL[pos] = (uint16_t)j;
+        }
       });
-  block_build_kdtree<uint16_t, false, false>(FC, C, n, P, T, 0);
+  // more features than this launch holds: the F = C launch takes the row;
+  // that launch skips the rows this one did
+  if (n > F || n <= done_le) return;  // uniform
+  block_build_kdtree<uint16_t, false, false>(FC, F, n, P, T, 0);
   // the tree in position order, in place: every old value is read into
   // registers before the barrier, then written to its position
   {
@@ -831,8 +845,8 @@ __global__ __launch_bounds__(NT) void k_rows_match_lean(
       if (pos < n) {
         const int e = P[pos];
         hx[u] = FC[e];
-        hy[u] = FC[C + e];
-        hz[u] = FC[2 * C + e];
+        hy[u] = FC[F + e];
+        hz[u] = FC[2 * F + e];
         hc[u] = FCOL[e];
       }
     }
@@ -842,8 +856,8 @@ __global__ __launch_bounds__(NT) void k_rows_match_lean(
       const int pos = (int)threadIdx.x + u * NT;
       if (pos < n) {
         FC[pos] = hx[u];
-        FC[C + pos] = hy[u];
-        FC[2 * C + pos] = hz[u];
+        FC[F + pos] = hy[u];
+        FC[2 * F + pos] = hz[u];
         T[pos] = hc[u];
       }
     }
@@ -864,12 +878,12 @@ __global__ __launch_bounds__(NT) void k_rows_match_lean(
   const int nq = block_compact(
       C, scan, [&](int j) { return P[j] != 0; },
       [&](int j, int pos) { QL[pos] = (uint16_t)j; });
-  const double *TX = FC, *TY = FC + C, *TZ = FC + 2 * C;
-  for (int i = threadIdx.x; i < nq; i += NT) {
+  const double *TX = FC, *TY = FC + F, *TZ = FC + 2 * F;
+  for (int i = threadIdx.x; i < nq && (int)threadIdx.x < walkers; i += walkers) {
     const int c = QL[i];
     int bpos;
     double bd;
-    kd_query(TX, TY, TZ, n, sg[3 * c], sg[3 * c + 1], sg[3 * c + 2], stk + threadIdx.x, NT,
+    kd_query(TX, TY, TZ, n, sg[3 * c], sg[3 * c + 1], sg[3 * c + 2], stk + threadIdx.x, walkers,
              &bpos, &bd);
     nn_idx[rowoff + c] = bpos >= 0 ? pair_row0 + canon_col(TX, TY, TZ, T, n, bpos) : -1;
     nn_dist[rowoff + c] = bd;
@@ -2653,11 +2667,19 @@ int rows_match_launch(navgpu_ctx *ctx, const double *src, const double *tgt, int
     tgt_mask = nullptr;
   }
   if (lean) {
-    const int lds = rows_lean_lds(C, 256);
-    RC(set_lds(k_rows_match_lean<256>, lds));
+    const int walkers = rows_lean_walkers(tie != nullptr, 256);
+    const int F1 = std::min(C, kLeanF);
+    int lds = rows_lean_lds(C, F1, walkers);
+    RC(set_lds(k_rows_match_lean<256>, std::max(lds, rows_lean_lds(C, C, walkers))));
     hipLaunchKernelGGL(k_rows_match_lean<256>, dim3(rows), dim3(256), lds, ctx->stream, src,
-                       tgt, R, C, src_mask, tgt_mask, nn_idx, nn_dist, tie, S);
+                       tgt, R, C, src_mask, tgt_mask, nn_idx, nn_dist, tie, S, F1, -1);
     CHECK_LAUNCH("k_rows_match_lean");
+    if (F1 < C) {  // the rows with more than F1 features
+      lds = rows_lean_lds(C, C, walkers);
+      hipLaunchKernelGGL(k_rows_match_lean<256>, dim3(rows), dim3(256), lds, ctx->stream, src,
+                         tgt, R, C, src_mask, tgt_mask, nn_idx, nn_dist, tie, S, C, F1);
+      CHECK_LAUNCH("k_rows_match_lean");
+    }
     return NAVGPU_OK;
   }
   const RowsLds L = rows_lds(C, kRowsBlock, true);

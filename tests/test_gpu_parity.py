@@ -580,6 +580,20 @@ def test_rows_match_k2_matches_reference_digest(gpu, golden, tag, integer):
     assert sha(d) == str(dg[f"k2{tag}_nnd"]), "distances differ from the reference"
 
 
+@pytest.mark.parametrize("C", [1, 2, 3, 4, 5, 6, 59, 60, 61, 63, 64, 65, 119, 120, 121, 241, 1000])
+def test_curvature_segment_edges(gpu, orc, C):
+    """k_curvature covers a row with waves of 60 output columns and a
+    2-column halo: row widths around the segment and block edges (and rows
+    too short for any curvature) against the oracle."""
+    rng = np.random.default_rng(C)
+    pts = rng.uniform(-2000, 2000, (5, C, 3))
+    pts[1] = np.round(pts[1])
+    m_ref, c_ref = orc.extract_feature(pts, want_curv=True)
+    m, cv = gpu.curvature(pts, want_curv=True)
+    _eq(m, m_ref, f"C={C} mask")
+    _eq(cv, c_ref, f"C={C} curvature")
+
+
 def test_curvature_k3_shape_bit_exact(gpu, orc):
     """R1 at the K3 shape: both 512x2048 clouds, mask and f64 value."""
     from navslam.synth import uniform_pair
