@@ -775,8 +775,9 @@ __global__ __launch_bounds__(kRowsBlock) void k_rows_match(
 constexpr int kLeanMaxC = 2048;  // in-place permutation: <= kLeanMaxC / NT per thread
 // (r3) the SoA features are sized for F <= C of them: a tie pass runs first
 // at F = kLeanF (three rows per CU instead of two), then again at F = C for
-// the rows whose feature count exceeded it (the others return at once); tree
-// walks, only the tied queries' there, take one wave
+// the rows whose feature count exceeded it (flagged in `over` by the first
+// launch; the others return at once); tree walks, only the tied queries'
+// there, take one wave
 constexpr int kLeanF = 1536;
 
 __host__ __device__ inline int rows_lean_walkers(bool tie, int nt) { return tie ? kWave : nt; }
@@ -798,10 +799,11 @@ __global__ __launch_bounds__(NT) void k_rows_match_lean(
     const double *__restrict__ src, const double *__restrict__ tgt, int R,
     int C, int32_t *__restrict__ src_mask, int32_t *__restrict__ tgt_mask,
     int32_t *__restrict__ nn_idx, double *__restrict__ nn_dist,
-    const int32_t *__restrict__ tie, int S, int F, int done_le) {
+    const int32_t *__restrict__ tie, int S, int F, int32_t *__restrict__ over, int second) {
   constexpr int kHold = kLeanMaxC / NT;
   const int r = blockIdx.x;
   if (tie && !row_has_tie(tie, r, S)) return;  // uniform
+  if (second && !over[r]) return;              // the first launch did this row
   const size_t rowoff = (size_t)r * C;
   const int pair_row0 = (r % R) * C;
   const int walkers = rows_lean_walkers(tie != nullptr, NT);
@@ -830,9 +832,11 @@ __global__ __launch_bounds__(NT) void k_rows_match_lean(
           FCOL[pos] = (uint16_t)j;
         }
       });
-  // more features than this launch holds: the F = C launch takes the row;
-  // that launch skips the rows this one did
-  if (n > F || n <= done_le) return;  // uniform
+  // more features than this launch holds: the F = C launch takes the row
+  if (!second) {
+    if (threadIdx.x == 0) over[r] = n > F;
+    if (n > F) return;  // uniform
+  }
   block_build_kdtree<uint16_t, false, false>(FC, F, n, P, T, 0);
   // the tree in position order, in place: every old value is read into
   // registers before the barrier, then written to its position
@@ -2669,15 +2673,17 @@ int rows_match_launch(navgpu_ctx *ctx, const double *src, const double *tgt, int
   if (lean) {
     const int walkers = rows_lean_walkers(tie != nullptr, 256);
     const int F1 = std::min(C, kLeanF);
+    int32_t *over;
+    RC(ws(ctx, kOvf, rows, &over));
     int lds = rows_lean_lds(C, F1, walkers);
     RC(set_lds(k_rows_match_lean<256>, std::max(lds, rows_lean_lds(C, C, walkers))));
     hipLaunchKernelGGL(k_rows_match_lean<256>, dim3(rows), dim3(256), lds, ctx->stream, src,
-                       tgt, R, C, src_mask, tgt_mask, nn_idx, nn_dist, tie, S, F1, -1);
+                       tgt, R, C, src_mask, tgt_mask, nn_idx, nn_dist, tie, S, F1, over, 0);
     CHECK_LAUNCH("k_rows_match_lean");
     if (F1 < C) {  // the rows with more than F1 features
       lds = rows_lean_lds(C, C, walkers);
       hipLaunchKernelGGL(k_rows_match_lean<256>, dim3(rows), dim3(256), lds, ctx->stream, src,
-                         tgt, R, C, src_mask, tgt_mask, nn_idx, nn_dist, tie, S, C, F1);
+                         tgt, R, C, src_mask, tgt_mask, nn_idx, nn_dist, tie, S, C, over, 1);
       CHECK_LAUNCH("k_rows_match_lean");
     }
     return NAVGPU_OK;
