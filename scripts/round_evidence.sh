@@ -27,6 +27,10 @@ fi
 export TMPDIR=/tmp
 Q="--no-cpu-baseline --no-traffic-json --no-stream-copy"
 step trace_k3 600 rocprofv3 --kernel-trace --stats -d "$OUT/trace_k3" -o run --output-format csv -- python3 bench.py --steps 20 --warmup 3 $Q --json-out "$OUT/bench_k3_traced.json"
+# one pair at a time: the trace's per-launch kernel sums and the line's HIP
+# events time the same isolated kernels
+step trace_k3_iso 600 rocprofv3 --kernel-trace --stats -d "$OUT/trace_k3_iso" -o run --output-format csv -- python3 bench.py --inflight 1 --steps 20 --warmup 3 $Q --json-out "$OUT/bench_k3_iso_traced.json"
+step trace_check 60 python3 scripts/trace_check.py "$(find "$OUT/trace_k3_iso" -name "*kernel_stats.csv" | head -1)" "$OUT/bench_k3_iso_traced.json" "$OUT/trace_check_k3.json"
 pmc() {  # pmc <w> <traffic args> -- <bench args>
   local w=$1; shift
   local targs=()

@@ -1,0 +1,36 @@
+"""Cross-check of a K3 bench line against the rocprofv3 kernel trace of the
+same run: per launch of k_knn<K>, the summed durations of the index build
+kernels, of the query-stage kernels and of the curvature, beside the line's
+HIP-event kernel_us (their span on the context's stream).
+
+usage: trace_check.py KERNEL_STATS_CSV BENCH_JSON OUT_JSON"""
+import csv
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from bench import BUILD_KERNELS, QUERY_KERNELS  # noqa: E402
+
+stats, line, out = sys.argv[1:4]
+rows = list(csv.DictReader(open(stats)))
+b = json.load(open(line))
+launches = sum(int(r["Calls"]) for r in rows if "k_knn<" in r["Name"])
+
+
+def per_launch(keys):
+    ns = sum(float(r["TotalDurationNs"]) for r in rows if any(k in r["Name"] for k in keys))
+    return round(ns / max(launches, 1) / 1e3, 2)
+
+
+rec = {"launches": launches,
+       "trace_us": {"knn_build": per_launch(BUILD_KERNELS),
+                    "knn_query": per_launch(QUERY_KERNELS),
+                    "curvature": per_launch(("k_curvature",))},
+       "line_kernel_us": b.get("kernel_us"),
+       "pairs_in_flight": b["config"].get("pairs_in_flight")}
+rec["ratio_line_over_trace"] = {k: round(b["kernel_us"][k] / v, 4)
+                                for k, v in rec["trace_us"].items() if v and k in b["kernel_us"]}
+with open(out, "w") as f:
+    json.dump(rec, f, indent=1)
+print(json.dumps(rec))
