@@ -205,7 +205,7 @@ int navgpu_pair_knn_dev(navgpu_ctx *ctx, const double *src, const double *tgt,
 /* ---- R5 for one arbitrary point array (kdtree.h buildKDTree) ------------
  * pts: n points (AoS), permuted in place into the reference's buildKDTree
  * order for a root at depth `depth0` (axis = (depth0 + level) % 3).
- * n < 2^30 and at most 2^15 windows per level (about 370M points; larger n
+ * n < 2^30 and at most 2^15 windows per level (about 383M points; larger n
  * returns NAVGPU_ERANGE). Up to ~5.7k points the build runs in one
  * workgroup's LDS.
  * Larger arrays run the reference's Lomuto passes grid-wide, level by level

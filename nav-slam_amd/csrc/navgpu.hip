@@ -2753,7 +2753,10 @@ int navgpu_rows_match_host(navgpu_ctx *ctx, const double *src,
 // ------------------------------------------------- kdtree.h buildKDTree
 int navgpu_kd_build_dev(navgpu_ctx *ctx, double *pts, size_t n, int depth0) {
   ARG_CHECK(ctx && depth0 >= 0);
-  ARG_CHECK(n < ((size_t)1 << 30));
+  if (n >= ((size_t)1 << 30)) {
+    set_err("kd_build: %zu points (at most 2^30 - 1)", n);
+    return NAVGPU_ERANGE;
+  }
   if (n < 2) return NAVGPU_OK;  // kdtree.c:22: nothing to permute
   ARG_CHECK(pts);
   const int ni = (int)n;
@@ -2766,17 +2769,24 @@ int navgpu_kd_build_dev(navgpu_ctx *ctx, double *pts, size_t n, int depth0) {
     CHECK_LAUNCH("k_kd_build_lds");
     return NAVGPU_OK;
   }
-  double *fc;
-  uint32_t *P, *T;
-  RC(ws(ctx, kKdFc, 3 * n, &fc));
-  RC(ws(ctx, kKdP, n, &P));
-  RC(ws(ctx, kKdT, n, &T));
   // levels above the leaves: until every subarray (<= ceil(n / 2^L)) fits
   // the LDS build of k_kd_leaves
   int L = 0;
   while (L < 30 && !(((n + ((size_t)1 << L) - 1) >> L) <= 65535 &&
                      kd_build_lds_bytes((int)((n + ((size_t)1 << L) - 1) >> L)) <= lds_limit()))
     ++L;
+  const int nWmax = 1 << std::max(0, L - 1);
+  // the selection kernels put a level's windows on grid.y (checked before
+  // any workspace is sized for n)
+  if (nWmax > 65535) {
+    set_err("kd_build: %zu points need %d windows per level (grid.y limit 65535)", n, nWmax);
+    return NAVGPU_ERANGE;
+  }
+  double *fc;
+  uint32_t *P, *T;
+  RC(ws(ctx, kKdFc, 3 * n, &fc));
+  RC(ws(ctx, kKdP, n, &P));
+  RC(ws(ctx, kKdT, n, &T));
   if (getenv("NAVGPU_KD_ONE_WG") || L >= 24) {  // the single-workgroup build (reference for tests)
     hipLaunchKernelGGL(k_kd_build_global, dim3(1), dim3(1024), 0, ctx->stream,
                        pts, ni, depth0 % 3, fc, P, T);
@@ -2793,12 +2803,6 @@ int navgpu_kd_build_dev(navgpu_ctx *ctx, double *pts, size_t n, int depth0) {
   const int kRounds = 2;  // 64 hops, then 64 more of the compressed chains;
                           // scatter follows whatever is left
   int32_t *stbuf;
-  const int nWmax = 1 << std::max(0, L - 1);
-  // the selection kernels put a level's windows on grid.y
-  if (nWmax > 65535) {
-    set_err("kd_build: %zu points need %d windows per level (grid.y limit 65535)", n, nWmax);
-    return NAVGPU_ERANGE;
-  }
   // per-level chunk counters: nW windows x chunks of one window, at most
   // about n / kSelChunk + nW at any level (not nWmax x all chunks of n)
   size_t ncnt = 0;

@@ -789,6 +789,44 @@ def test_rows_corr_matches_reference_dedup(gpu, orc, integer_mm):
     assert ek.sum() > 0 and (ek.sum() < (pos.cpu().numpy() >= 0).sum() or not integer_mm)
 
 
+@pytest.mark.parametrize("n", [400_000_000, 1 << 30])
+def test_kd_build_beyond_limit_returns_erange(gpu, n):
+    """navgpu_kd_build_dev (include/navgpu.h): above about 383M points a
+    level holds more than 65535 windows (grid.y of the selection kernels),
+    and n >= 2^30 overflows the int positions: both return NAVGPU_ERANGE
+    (-4) before any workspace is sized for n or any point is read (ADVICE
+    r2)."""
+    import torch
+    from navslam.gpu import NavGpuError
+    pts = torch.zeros((4, 3), dtype=torch.float64, device="cuda")
+    with pytest.raises(NavGpuError, match=r"\(-4\)"):
+        gpu.kd_build_dev(pts, n)
+    gpu.sync()
+
+
+def test_rows_corr_rows_beyond_lds_return_erange(gpu):
+    """The dedup kernels hold a row's hash (>= 2C slots) in LDS: rows wider
+    than 2048 columns exceed the device's LDS and must return NAVGPU_ERANGE
+    (-4) before any launch, not fail inside HIP."""
+    import torch
+    from navslam.gpu import NavGpuError
+    R, Cc = 2, 2112
+    dev = torch.device("cuda", 0)
+    pts = torch.zeros((R, Cc, 3), dtype=torch.float64, device=dev)
+    tn = torch.zeros(R, dtype=torch.int32, device=dev)
+    pos = torch.full((R, Cc), -1, dtype=torch.int32, device=dev)
+    dist = torch.full((R, Cc), float("inf"), dtype=torch.float64, device=dev)
+    keep = torch.empty((R, Cc), dtype=torch.int32, device=dev)
+    sums = torch.empty((R, 6), dtype=torch.float64, device=dev)
+    with pytest.raises(NavGpuError, match=r"\(-4\)"):
+        gpu.rows_corr_dev(pts, tn, pos, dist, pts, R, Cc, keep, sums)
+    lst = torch.empty((R * Cc, 7), dtype=torch.float64, device=dev)
+    count = torch.zeros(1, dtype=torch.int32, device=dev)
+    with pytest.raises(NavGpuError, match=r"\(-4\)"):
+        gpu.rows_corr_list_dev(pts, tn, pos, dist, pts, R, Cc, lst, count)
+    gpu.sync()
+
+
 @pytest.mark.parametrize("R,Cc", [(24, 640), (2100, 42)])
 def test_kd_rows_nodes_image_links_the_implicit_trees(gpu, R, Cc):
     """navgpu_kd_rows_nodes_dev: the KDNode image (utils/kdtree.h:7-11) of the
