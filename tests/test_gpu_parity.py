@@ -467,6 +467,48 @@ def test_knn_hard_cases(gpu, orc, k):
         _eq(gd, rd, f"{name} k={k} dist")
 
 
+@pytest.mark.parametrize("sx", [1, 2, 3, 8])
+def test_knn_cell_slicing_variants(orc, sx, monkeypatch):
+    """NAVGPU_KNN_SX (x cells per h; default 4) reshapes every tile, block
+    and certificate reach: each setting gives the brute-force answer, on
+    uniform, integer-mm and clustered data, k = 2, 8 and 13."""
+    from navslam.gpu import NavGpu
+    monkeypatch.setenv("NAVGPU_KNN_SX", str(sx))
+    g = NavGpu(0)
+    try:
+        rng = np.random.default_rng(40 + sx)
+        cases = [(rng.uniform(0, 800, (6000, 3)), rng.uniform(-20, 820, (2500, 3))),
+                 (np.round(rng.uniform(0, 30, (5000, 3))), np.round(rng.uniform(0, 30, (1500, 3)))),
+                 (_clustered(rng, 8000, 4, 1.0, 500.0), rng.uniform(0, 500, (1200, 3)))]
+        for ci, (t, q) in enumerate(cases):
+            for k in (2, 8, 13):
+                ri, rd = orc.knn_brute(t, q, k)
+                gi, gd = g.knn(t, q, k)
+                _eq(gi, ri, f"sx={sx} case {ci} k={k} idx")
+                _eq(gd, rd, f"sx={sx} case {ci} k={k} dist")
+    finally:
+        g.close()
+
+
+def test_knn_huge_coordinates(gpu, orc):
+    """Coordinates past the f32 offsets' certified range (|x| ~ 1e18 mm) and a
+    cloud spanning 1e-3 .. 1e15 mm: the certificate fails and the slow path
+    answers, exactly."""
+    rng = np.random.default_rng(77)
+    t = rng.uniform(-1, 1, (2000, 3)) * 1e18
+    q = rng.uniform(-1, 1, (300, 3)) * 1e18
+    ri, rd = orc.knn_brute(t, q, 8)
+    gi, gd = gpu.knn(t, q, 8)
+    _eq(gi, ri, "1e18 idx")
+    _eq(gd, rd, "1e18 dist")
+    t = np.concatenate([rng.uniform(0, 1e-3, (1500, 3)), rng.uniform(0, 1e15, (1500, 3))])
+    q = np.concatenate([rng.uniform(0, 1e-3, (200, 3)), rng.uniform(0, 1e15, (200, 3))])
+    ri, rd = orc.knn_brute(t, q, 4)
+    gi, gd = gpu.knn(t, q, 4)
+    _eq(gi, ri, "wide-range idx")
+    _eq(gd, rd, "wide-range dist")
+
+
 def test_knn_k1_agrees_with_reference_kd_distances(gpu, golden):
     for pts, perm, q, nn, nnd in _golden_sets(golden("kdtree")):
         if len(pts) == 0:
