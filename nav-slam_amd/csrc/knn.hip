@@ -1333,10 +1333,12 @@ int knn_stamps_take(unsigned long long *out16) {
 }
 }  // namespace nv
 
-// The k-NN call (navgpu_knn_dev): index build, query pass, slow pass; all on
-// the context's stream, nothing allocated once the workspace is warm.
+// The k-NN call (navgpu_knn_dev): index build on stream sb, then query pass
+// and slow pass on sq (sq waits for the build through `built` when the two
+// differ: the CU split); nothing allocated once the workspace is warm.
 static int knn_run(navgpu_ctx *ctx, const double *tgt, size_t nt, const double *queries,
-                   size_t nq, int k, int32_t *idx, double *dist) {
+                   size_t nq, int k, int32_t *idx, double *dist, hipStream_t sb,
+                   hipStream_t sq, hipEvent_t built) {
   ARG_CHECK(ctx && k >= 1 && k <= 16);
   ARG_CHECK(nt < (size_t)INT32_MAX / 2 && nq < (size_t)INT32_MAX / 2);
   if (!nq) return NAVGPU_OK;
@@ -1405,9 +1407,9 @@ static int knn_run(navgpu_ctx *ctx, const double *tgt, size_t nt, const double *
   J.s[1].sorted = nullptr;
   J.s[0].perm = nullptr;
   J.s[1].perm = qperm;
-  hipStream_t s = ctx->stream;
+  hipStream_t s = sb;
   {
-    TimedRegion tb(ctx, "knn_build");
+    TimedRegion tb(ctx, "knn_build", sb);
     if (nt) {
       hipLaunchKernelGGL(k_bbox_partial, dim3(nparts), dim3(256), 0, s, tgt, nt, part);
       CHECK_LAUNCH("k_bbox_partial");
@@ -1433,13 +1435,18 @@ static int knn_run(navgpu_ctx *ctx, const double *tgt, size_t nt, const double *
                        (const int *)bbase, nscan);
     CHECK_LAUNCH("k_bin_fine");
   }
+  if (sq != sb) {
+    HIP_TRY(hipEventRecord(built, sb));
+    HIP_TRY(hipStreamWaitEvent(sq, built, 0));
+    s = sq;
+  }
   KnnLists lists;
   RC(ws(ctx, kSlowQ, nq, &lists.slow_q));
   RC(ws(ctx, kSlowThr, nq, &lists.slow_thr));
   lists.n_unstaged = counters;
   lists.n_slow = counters + 1;
   lists.vec_out = ((uintptr_t)idx % 16 == 0 && (uintptr_t)dist % 16 == 0) ? 1 : 0;
-  TimedRegion tr(ctx, "knn_query");
+  TimedRegion tr(ctx, "knn_query", sq);
   // tiles are walked by a grid of 8 x nbx blocks (block b -> XCD b % 8, the
   // placement HW_REG_XCC_ID reports); more blocks than resident slots
   // balance the uneven tiles
@@ -1481,9 +1488,27 @@ static int knn_run(navgpu_ctx *ctx, const double *tgt, size_t nt, const double *
 
 extern "C" {
 
+// The CU split: fork from the context's stream into the build stream, run
+// the build there and the query on the query stream, join back. The fork
+// orders this call after everything before it on the context's stream,
+// including the previous call's join, so a context's workspace is never
+// rebuilt while its last query still reads it.
+static int knn_split(navgpu_ctx *ctx, const double *tgt, size_t nt, const double *queries,
+                     size_t nq, int k, int32_t *idx, double *dist) {
+  RC(ensure_split(ctx));
+  HIP_TRY(hipEventRecord(ctx->ev_fork, ctx->stream));
+  HIP_TRY(hipStreamWaitEvent(ctx->sb, ctx->ev_fork, 0));
+  RC(knn_run(ctx, tgt, nt, queries, nq, k, idx, dist, ctx->sb, ctx->sq, ctx->ev_built));
+  HIP_TRY(hipEventRecord(ctx->ev_join, ctx->sq));
+  HIP_TRY(hipStreamWaitEvent(ctx->stream, ctx->ev_join, 0));
+  return NAVGPU_OK;
+}
+
 int navgpu_knn_dev(navgpu_ctx *ctx, const double *tgt, size_t nt, const double *queries,
                    size_t nq, int k, int32_t *idx, double *dist) {
-  return knn_run(ctx, tgt, nt, queries, nq, k, idx, dist);
+  if (ctx && ctx->split_b > 0 && nq) return knn_split(ctx, tgt, nt, queries, nq, k, idx, dist);
+  ARG_CHECK(ctx);
+  return knn_run(ctx, tgt, nt, queries, nq, k, idx, dist, ctx->stream, ctx->stream, nullptr);
 }
 
 int navgpu_knn_host(navgpu_ctx *ctx, const double *tgt, size_t nt, const double *queries,
@@ -1514,6 +1539,34 @@ int navgpu_pair_knn_dev(navgpu_ctx *ctx, const double *src, const double *tgt, i
   if (!N) return NAVGPU_OK;
   ARG_CHECK(src && tgt);
   if (!src_mask && !tgt_mask) return navgpu_knn_dev(ctx, tgt, N, src, N, k, idx, dist);
+  if (ctx->split_b > 0) {
+    // the CU split (navgpu_set_cu_split): build on sb, query on sq, the
+    // curvature on either (split_curv); forked from and joined into the
+    // context's stream
+    RC(ensure_split(ctx));
+    HIP_TRY(hipEventRecord(ctx->ev_fork, ctx->stream));
+    HIP_TRY(hipStreamWaitEvent(ctx->sb, ctx->ev_fork, 0));
+    hipStream_t cs = ctx->split_curv ? ctx->sq : ctx->sb;
+    if (ctx->split_curv) {  // ahead of the query on sq: runs while the build does
+      HIP_TRY(hipStreamWaitEvent(ctx->sq, ctx->ev_fork, 0));
+      TimedRegion tr(ctx, "curvature", cs);
+      RC(launch_curvature(src_mask ? src : tgt, src_mask ? src_mask : tgt_mask, nullptr,
+                          src_mask && tgt_mask ? tgt : nullptr,
+                          src_mask && tgt_mask ? tgt_mask : nullptr, nullptr, R, C, cs));
+    }
+    RC(knn_run(ctx, tgt, N, src, N, k, idx, dist, ctx->sb, ctx->sq, ctx->ev_built));
+    if (!ctx->split_curv) {  // behind the build on sb: overlaps the query
+      TimedRegion tr(ctx, "curvature", cs);
+      RC(launch_curvature(src_mask ? src : tgt, src_mask ? src_mask : tgt_mask, nullptr,
+                          src_mask && tgt_mask ? tgt : nullptr,
+                          src_mask && tgt_mask ? tgt_mask : nullptr, nullptr, R, C, cs));
+      HIP_TRY(hipEventRecord(ctx->ev_curv, cs));
+      HIP_TRY(hipStreamWaitEvent(ctx->stream, ctx->ev_curv, 0));
+    }
+    HIP_TRY(hipEventRecord(ctx->ev_join, ctx->sq));
+    HIP_TRY(hipStreamWaitEvent(ctx->stream, ctx->ev_join, 0));
+    return NAVGPU_OK;
+  }
   // One curvature launch over both clouds, on a side stream forked from and
   // joined back into the context's stream: it is f64-bound and independent
   // of the (latency-bound) index build and query, so the two overlap.
@@ -1530,7 +1583,7 @@ int navgpu_pair_knn_dev(navgpu_ctx *ctx, const double *src, const double *tgt, i
       RC(launch_curvature(tgt, tgt_mask, nullptr, nullptr, nullptr, nullptr, R, C, ctx->aux));
   }
   HIP_TRY(hipEventRecord(ctx->ev_join, ctx->aux));
-  const int rc = knn_run(ctx, tgt, N, src, N, k, idx, dist);
+  const int rc = knn_run(ctx, tgt, N, src, N, k, idx, dist, ctx->stream, ctx->stream, nullptr);
   HIP_TRY(hipStreamWaitEvent(ctx->stream, ctx->ev_join, 0));  // join before returning
   return rc;
 }
