@@ -71,10 +71,6 @@ def parse():
                         "HBM-bound index build overlaps the previous pair's issue-bound "
                         "query (measured: 1 -> 0.345 ms/pair, 2 -> 0.294, 3 -> 0.294); "
                         "--graph needs --inflight 1")
-    p.add_argument("--cu-split", default="",
-                   help="k3: 'B[,Q[,C]]' -- index build on B CUs of every XCD, query pass on "
-                        "the next Q (default: the rest), curvature on the query side (C=1) "
-                        "or the build side (C=0); navgpu_set_cu_split. Empty: off")
     p.add_argument("--cpu-reps", type=int, default=5,
                    help="CPU baseline: timed repetitions (median), after one untimed warm-up")
     p.add_argument("--resident-pairs", type=int, default=9,
@@ -461,14 +457,6 @@ def main():
                        ((N, a.k), torch.float64)))
                 for _ in range(nf)]
         ctxs = [g] + extra
-        split = None
-        if a.cu_split:
-            v = [int(x) for x in a.cu_split.split(",")]
-            v += [0, 1][len(v) - 1:]  # defaults: Q = the rest, curvature on the query side
-            split = {"build_cus_per_xcd": v[0], "query_cus_per_xcd": v[1] or None,
-                     "curvature": "query side" if v[2] else "build side"}
-            for c in ctxs:
-                c.set_cu_split(v[0], v[1], bool(v[2]))
         turn = [0]
 
         def step():
@@ -507,8 +495,6 @@ def main():
         cfg_extra = {"points_per_cloud": N, "k": a.k, "pairs_per_gpu": 1, "mode": "global",
                      "pairs_in_flight": nf, "resident_pairs": res_pairs,
                      "resident_bytes": res_pairs * 2 * 24 * N}
-        if split:
-            cfg_extra["cu_split"] = split
     else:
         ctxs, iso_step, nf = [g], None, 1
         R = a.rows or 128
@@ -628,8 +614,6 @@ def main():
     # the timed region (K3 with pairs in flight only)
     kt_iso = None
     if iso_step is not None and nf > 1 and a.iso_steps > 0:
-        if a.workload == "k3" and a.cu_split:
-            g.set_cu_split(0)  # isolated = one pair at a time on the whole chip
         for _ in range(a.iso_steps):
             iso_step()
         torch.cuda.synchronize()

@@ -202,20 +202,6 @@ int navgpu_pair_knn_dev(navgpu_ctx *ctx, const double *src, const double *tgt,
                         int R, int C, int k, int32_t *src_mask,
                         int32_t *tgt_mask, int32_t *idx, double *dist);
 
-/* CU split of the global-mode calls (navgpu_knn_dev, navgpu_pair_knn_dev):
- * the index build runs on a stream masked to build_cus CUs of every XCD,
- * the query pass on a second one masked to the next query_cus (0 = the rest
- * of the XCD), and the pair path's curvature on the query side
- * (curv_on_query = 1) or the build side. Both calls still fork from and join
- * into the context's stream, so stream order and results are unchanged;
- * consecutive calls on two contexts then overlap one pair's build with the
- * other's query on disjoint CUs. The two masked streams are shared by every
- * context of the process with the same split. build_cus = 0 turns the split
- * off (the default; NAVGPU_CU_SPLIT="b,q[,curv]" sets it at creation).
- * Not part of the reference interface. */
-int navgpu_set_cu_split(navgpu_ctx *ctx, int build_cus, int query_cus,
-                        int curv_on_query);
-
 /* ---- R5 for one arbitrary point array (kdtree.h buildKDTree) ------------
  * pts: n points (AoS), permuted in place into the reference's buildKDTree
  * order for a root at depth `depth0` (axis = (depth0 + level) % 3).

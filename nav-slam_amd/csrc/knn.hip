@@ -446,47 +446,75 @@ __global__ __launch_bounds__(256) void k_bin_scatter(BinJob J, const GridParams 
 }
 
 // One bucket: count its points per cell (LDS), scan, write the cell starts,
-// then place every point (targets) or its bucketed position (queries). The
+// then place every point (targets) or its bucketed position (queries).
+// Queries of a bucket of at most kFineStage points (the usual case) are
+// staged: each output position gets its input slot in LDS (lslot) and the
+// positions are written in order, coalesced, instead of one scattered 4-B
+// store each (r3 A/B: build 107 -> 106 us; staging the targets' 32-B records
+// the same way measured 113 us: their LDS halves the resident blocks, and a
+// scattered 32-B record store is already a whole sector). Otherwise the
 // first kBinFineHold * blockDim points stay in registers between the count
-// and the placement (one global read, not two); a larger bucket re-reads the
-// rest.
+// and the placement and the rest are re-read.
+constexpr int kFineStage = 2048;
+constexpr int kFineStageHold = kFineStage / kBinFineThreads;
+// dynamic LDS: cnt[2^shift], then lslot[kFineStage] when queries are staged
+constexpr size_t fine_lds_bytes(int shift, bool stage_q) {
+  return ((size_t)4 << shift) + (stage_q ? (size_t)kFineStage * sizeof(uint16_t) : 0);
+}
 __global__ __launch_bounds__(kBinFineThreads) void k_bin_fine(BinJob J,
                                                               const GridParams *__restrict__ gp,
                                                               const int *__restrict__ bbase,
-                                                              int nscan) {
-  extern __shared__ int cnt[];  // 2^shift
+                                                              int nscan, int qstage) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char fine_lds[];
+  int *cnt = (int *)fine_lds;                                        // 2^shift
+  uint16_t *lslot = (uint16_t *)(fine_lds + ((size_t)4 << J.shift));  // qstage
   __shared__ int scratch[40];
   const int side = blockIdx.x >= J.nb ? 1 : 0;
   const int b = blockIdx.x - (side ? J.nb : 0);
   const BinSide S = J.s[side];
   const int ncell = 1 << J.shift, base = b << J.shift;
   const int lo = bbase[side * (J.nb + 1) + b], hi = bbase[side * (J.nb + 1) + b + 1];
+  const int n = hi - lo;
+  const bool staged = side && n <= qstage;
   const BinPt *src = S.bin;
-  for (int j = threadIdx.x; j < ncell; j += blockDim.x) cnt[j] = 0;
+  const int bd = (int)blockDim.x, tid = (int)threadIdx.x;
+  for (int j = tid; j < ncell; j += bd) cnt[j] = 0;
   __syncthreads();
-  // queries hold only their cell (the placement writes the position)
+  // unstaged: queries hold only their cell (the placement writes the position)
   BinPt hold[kBinFineHold];
-  const int bd = (int)blockDim.x, held_end = min(hi, lo + kBinFineHold * bd);
+  int scell[kFineStageHold];
+  const int held_end = min(hi, lo + kBinFineHold * bd);
+  if (staged) {
 #pragma unroll
-  for (int u = 0; u < kBinFineHold; ++u) {
-    const int i = lo + u * bd + (int)threadIdx.x;
-    if (i < held_end) {
-      if (side)
-        hold[u].cell = src[i].cell;
-      else
-        hold[u] = src[i];
+    for (int u = 0; u < kFineStageHold; ++u) {
+      const int sl = u * bd + tid;
+      if (sl < n) scell[u] = src[lo + sl].cell;
     }
-  }
 #pragma unroll
-  for (int u = 0; u < kBinFineHold; ++u) {
-    const int i = lo + u * bd + (int)threadIdx.x;
-    if (i < held_end) atomicAdd(&cnt[hold[u].cell - base], 1);
+    for (int u = 0; u < kFineStageHold; ++u)
+      if (u * bd + tid < n) atomicAdd(&cnt[scell[u] - base], 1);
+  } else {
+#pragma unroll
+    for (int u = 0; u < kBinFineHold; ++u) {
+      const int i = lo + u * bd + tid;
+      if (i < held_end) {
+        if (side)
+          hold[u].cell = src[i].cell;
+        else
+          hold[u] = src[i];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < kBinFineHold; ++u) {
+      const int i = lo + u * bd + tid;
+      if (i < held_end) atomicAdd(&cnt[hold[u].cell - base], 1);
+    }
+    for (int i = held_end + tid; i < hi; i += bd) atomicAdd(&cnt[src[i].cell - base], 1);
   }
-  for (int i = held_end + (int)threadIdx.x; i < hi; i += bd) atomicAdd(&cnt[src[i].cell - base], 1);
   __syncthreads();
   // exclusive scan over the bucket's cells: each thread owns a contiguous run
   const int per = ncell / bd;  // ncell is a multiple of the block size
-  const int j0 = (int)threadIdx.x * per;
+  const int j0 = tid * per;
   int sum = 0;
   for (int u = 0; u < per; ++u) sum += cnt[j0 + u];
   int total;
@@ -499,6 +527,16 @@ __global__ __launch_bounds__(kBinFineThreads) void k_bin_fine(BinJob J,
   }
   __syncthreads();
   const int g0 = gp->g[0];
+  if (staged) {
+#pragma unroll
+    for (int u = 0; u < kFineStageHold; ++u) {
+      const int sl = u * bd + tid;
+      if (sl < n) lslot[atomicAdd(&cnt[scell[u] - base], 1) - lo] = (uint16_t)sl;
+    }
+    __syncthreads();
+    for (int j = tid; j < n; j += bd) S.perm[lo + j] = lo + lslot[j];
+    return;
+  }
   auto place = [&](const BinPt &e, int i) {
     const int pos = atomicAdd(&cnt[e.cell - base], 1);
     if (side) {
@@ -515,10 +553,10 @@ __global__ __launch_bounds__(kBinFineThreads) void k_bin_fine(BinJob J,
   };
 #pragma unroll
   for (int u = 0; u < kBinFineHold; ++u) {
-    const int i = lo + u * bd + (int)threadIdx.x;
+    const int i = lo + u * bd + tid;
     if (i < held_end) place(hold[u], i);
   }
-  for (int i = held_end + (int)threadIdx.x; i < hi; i += bd) place(src[i], i);
+  for (int i = held_end + tid; i < hi; i += bd) place(src[i], i);
 }
 
 // ============================================================ k-NN helpers
@@ -1333,12 +1371,10 @@ int knn_stamps_take(unsigned long long *out16) {
 }
 }  // namespace nv
 
-// The k-NN call (navgpu_knn_dev): index build on stream sb, then query pass
-// and slow pass on sq (sq waits for the build through `built` when the two
-// differ: the CU split); nothing allocated once the workspace is warm.
+// The k-NN call (navgpu_knn_dev): index build, query pass, slow pass; all on
+// the context's stream, nothing allocated once the workspace is warm.
 static int knn_run(navgpu_ctx *ctx, const double *tgt, size_t nt, const double *queries,
-                   size_t nq, int k, int32_t *idx, double *dist, hipStream_t sb,
-                   hipStream_t sq, hipEvent_t built) {
+                   size_t nq, int k, int32_t *idx, double *dist) {
   ARG_CHECK(ctx && k >= 1 && k <= 16);
   ARG_CHECK(nt < (size_t)INT32_MAX / 2 && nq < (size_t)INT32_MAX / 2);
   if (!nq) return NAVGPU_OK;
@@ -1407,9 +1443,9 @@ static int knn_run(navgpu_ctx *ctx, const double *tgt, size_t nt, const double *
   J.s[1].sorted = nullptr;
   J.s[0].perm = nullptr;
   J.s[1].perm = qperm;
-  hipStream_t s = sb;
+  hipStream_t s = ctx->stream;
   {
-    TimedRegion tb(ctx, "knn_build", sb);
+    TimedRegion tb(ctx, "knn_build");
     if (nt) {
       hipLaunchKernelGGL(k_bbox_partial, dim3(nparts), dim3(256), 0, s, tgt, nt, part);
       CHECK_LAUNCH("k_bbox_partial");
@@ -1427,18 +1463,15 @@ static int knn_run(navgpu_ctx *ctx, const double *tgt, size_t nt, const double *
     hipLaunchKernelGGL(k_bin_scatter, gb, dim3(256), 0, s, J, gp, (const int *)tab,
                        (const int *)btot, bbase);
     CHECK_LAUNCH("k_bin_scatter");
-    const size_t lds = (size_t)4 << shift;
+    // staged query placement when its LDS fits beside a 2^shift count table
+    const bool st_q = fine_lds_bytes(shift, true) <= 144 * 1024;
+    const size_t lds = fine_lds_bytes(shift, st_q);
     if (lds > 48 * 1024)
       HIP_TRY(hipFuncSetAttribute((const void *)k_bin_fine,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     hipLaunchKernelGGL(k_bin_fine, dim3(2 * J.nb), dim3(kBinFineThreads), lds, s, J, gp,
-                       (const int *)bbase, nscan);
+                       (const int *)bbase, nscan, st_q ? kFineStage : 0);
     CHECK_LAUNCH("k_bin_fine");
-  }
-  if (sq != sb) {
-    HIP_TRY(hipEventRecord(built, sb));
-    HIP_TRY(hipStreamWaitEvent(sq, built, 0));
-    s = sq;
   }
   KnnLists lists;
   RC(ws(ctx, kSlowQ, nq, &lists.slow_q));
@@ -1446,7 +1479,7 @@ static int knn_run(navgpu_ctx *ctx, const double *tgt, size_t nt, const double *
   lists.n_unstaged = counters;
   lists.n_slow = counters + 1;
   lists.vec_out = ((uintptr_t)idx % 16 == 0 && (uintptr_t)dist % 16 == 0) ? 1 : 0;
-  TimedRegion tr(ctx, "knn_query", sq);
+  TimedRegion tr(ctx, "knn_query");
   // tiles are walked by a grid of 8 x nbx blocks (block b -> XCD b % 8, the
   // placement HW_REG_XCC_ID reports); more blocks than resident slots
   // balance the uneven tiles
@@ -1488,27 +1521,9 @@ static int knn_run(navgpu_ctx *ctx, const double *tgt, size_t nt, const double *
 
 extern "C" {
 
-// The CU split: fork from the context's stream into the build stream, run
-// the build there and the query on the query stream, join back. The fork
-// orders this call after everything before it on the context's stream,
-// including the previous call's join, so a context's workspace is never
-// rebuilt while its last query still reads it.
-static int knn_split(navgpu_ctx *ctx, const double *tgt, size_t nt, const double *queries,
-                     size_t nq, int k, int32_t *idx, double *dist) {
-  RC(ensure_split(ctx));
-  HIP_TRY(hipEventRecord(ctx->ev_fork, ctx->stream));
-  HIP_TRY(hipStreamWaitEvent(ctx->sb, ctx->ev_fork, 0));
-  RC(knn_run(ctx, tgt, nt, queries, nq, k, idx, dist, ctx->sb, ctx->sq, ctx->ev_built));
-  HIP_TRY(hipEventRecord(ctx->ev_join, ctx->sq));
-  HIP_TRY(hipStreamWaitEvent(ctx->stream, ctx->ev_join, 0));
-  return NAVGPU_OK;
-}
-
 int navgpu_knn_dev(navgpu_ctx *ctx, const double *tgt, size_t nt, const double *queries,
                    size_t nq, int k, int32_t *idx, double *dist) {
-  if (ctx && ctx->split_b > 0 && nq) return knn_split(ctx, tgt, nt, queries, nq, k, idx, dist);
-  ARG_CHECK(ctx);
-  return knn_run(ctx, tgt, nt, queries, nq, k, idx, dist, ctx->stream, ctx->stream, nullptr);
+  return knn_run(ctx, tgt, nt, queries, nq, k, idx, dist);
 }
 
 int navgpu_knn_host(navgpu_ctx *ctx, const double *tgt, size_t nt, const double *queries,
@@ -1539,34 +1554,6 @@ int navgpu_pair_knn_dev(navgpu_ctx *ctx, const double *src, const double *tgt, i
   if (!N) return NAVGPU_OK;
   ARG_CHECK(src && tgt);
   if (!src_mask && !tgt_mask) return navgpu_knn_dev(ctx, tgt, N, src, N, k, idx, dist);
-  if (ctx->split_b > 0) {
-    // the CU split (navgpu_set_cu_split): build on sb, query on sq, the
-    // curvature on either (split_curv); forked from and joined into the
-    // context's stream
-    RC(ensure_split(ctx));
-    HIP_TRY(hipEventRecord(ctx->ev_fork, ctx->stream));
-    HIP_TRY(hipStreamWaitEvent(ctx->sb, ctx->ev_fork, 0));
-    hipStream_t cs = ctx->split_curv ? ctx->sq : ctx->sb;
-    if (ctx->split_curv) {  // ahead of the query on sq: runs while the build does
-      HIP_TRY(hipStreamWaitEvent(ctx->sq, ctx->ev_fork, 0));
-      TimedRegion tr(ctx, "curvature", cs);
-      RC(launch_curvature(src_mask ? src : tgt, src_mask ? src_mask : tgt_mask, nullptr,
-                          src_mask && tgt_mask ? tgt : nullptr,
-                          src_mask && tgt_mask ? tgt_mask : nullptr, nullptr, R, C, cs));
-    }
-    RC(knn_run(ctx, tgt, N, src, N, k, idx, dist, ctx->sb, ctx->sq, ctx->ev_built));
-    if (!ctx->split_curv) {  // behind the build on sb: overlaps the query
-      TimedRegion tr(ctx, "curvature", cs);
-      RC(launch_curvature(src_mask ? src : tgt, src_mask ? src_mask : tgt_mask, nullptr,
-                          src_mask && tgt_mask ? tgt : nullptr,
-                          src_mask && tgt_mask ? tgt_mask : nullptr, nullptr, R, C, cs));
-      HIP_TRY(hipEventRecord(ctx->ev_curv, cs));
-      HIP_TRY(hipStreamWaitEvent(ctx->stream, ctx->ev_curv, 0));
-    }
-    HIP_TRY(hipEventRecord(ctx->ev_join, ctx->sq));
-    HIP_TRY(hipStreamWaitEvent(ctx->stream, ctx->ev_join, 0));
-    return NAVGPU_OK;
-  }
   // One curvature launch over both clouds, on a side stream forked from and
   // joined back into the context's stream: it is f64-bound and independent
   // of the (latency-bound) index build and query, so the two overlap.
@@ -1583,7 +1570,7 @@ int navgpu_pair_knn_dev(navgpu_ctx *ctx, const double *src, const double *tgt, i
       RC(launch_curvature(tgt, tgt_mask, nullptr, nullptr, nullptr, nullptr, R, C, ctx->aux));
   }
   HIP_TRY(hipEventRecord(ctx->ev_join, ctx->aux));
-  const int rc = knn_run(ctx, tgt, N, src, N, k, idx, dist, ctx->stream, ctx->stream, nullptr);
+  const int rc = knn_run(ctx, tgt, N, src, N, k, idx, dist);
   HIP_TRY(hipStreamWaitEvent(ctx->stream, ctx->ev_join, 0));  // join before returning
   return rc;
 }

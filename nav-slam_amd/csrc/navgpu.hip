@@ -2071,58 +2071,6 @@ int ensure_aux(navgpu_ctx *ctx) {
   return NAVGPU_OK;
 }
 
-// ---- CU split (navgpu_set_cu_split) -----------------------------------------
-// Two CU-masked streams per (device, split), shared by all contexts of the
-// process: the HSA queue of a masked stream is its own (it does not come out
-// of the GPU_MAX_HW_QUEUES pool), so contexts must not each make a pair.
-// Mask bit i is CU i / nx of XCD i % nx (the KFD maps a multi-XCD mask
-// interleaved; bench_micro/cu_mask.hip checks it on the box), so taking CUs
-// [c0, c1) of every XCD never leaves an XCD without CUs.
-namespace {
-struct SplitKey {
-  int dev, b, q;
-  bool operator<(const SplitKey &o) const {
-    return dev != o.dev ? dev < o.dev : (b != o.b ? b < o.b : q < o.q);
-  }
-};
-std::map<SplitKey, std::pair<hipStream_t, hipStream_t>> g_split;
-
-int split_xcds(int ncu) { return (ncu >= 64 && ncu % 8 == 0) ? 8 : 1; }
-
-int masked_stream(int ncu, int c0, int c1, hipStream_t *out) {
-  const int nx = split_xcds(ncu);
-  std::vector<uint32_t> m((ncu + 31) / 32, 0u);
-  for (int i = 0; i < ncu; ++i) {
-    const int c = i / nx;
-    if (c >= c0 && c < c1) m[i / 32] |= 1u << (i % 32);
-  }
-  HIP_TRY(hipExtStreamCreateWithCUMask(out, (uint32_t)m.size(), m.data()));
-  return NAVGPU_OK;
-}
-}  // namespace
-
-int ensure_split(navgpu_ctx *ctx) {
-  RC(ensure_aux(ctx));
-  if (!ctx->ev_built) {
-    HIP_TRY(hipEventCreateWithFlags(&ctx->ev_built, hipEventDisableTiming));
-    HIP_TRY(hipEventCreateWithFlags(&ctx->ev_curv, hipEventDisableTiming));
-  }
-  if (ctx->sb) return NAVGPU_OK;
-  const SplitKey key{ctx->device, ctx->split_b, ctx->split_q};
-  auto it = g_split.find(key);
-  if (it == g_split.end()) {
-    int ncu = 0;
-    HIP_TRY(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, ctx->device));
-    hipStream_t sb, sq;
-    RC(masked_stream(ncu, 0, ctx->split_b, &sb));
-    RC(masked_stream(ncu, ctx->split_b, ctx->split_b + ctx->split_q, &sq));
-    it = g_split.emplace(key, std::make_pair(sb, sq)).first;
-  }
-  ctx->sb = it->second.first;
-  ctx->sq = it->second.second;
-  return NAVGPU_OK;
-}
-
 int launch_curvature(const double *pts0, int32_t *mask0, double *curv0,
                      const double *pts1, int32_t *mask1, double *curv1, int R, int C,
                      hipStream_t stream) {
@@ -2214,20 +2162,6 @@ int navgpu_create(int device, void *stream, navgpu_ctx **out) {
     const double v = atof(o);
     if (v >= 1.0 && v < 1e6) c->knn_lambda = v;
   }
-  if (const char *o = getenv("NAVGPU_CU_SPLIT")) {  // "b,q[,curv]" (navgpu_set_cu_split)
-    int b = 0, q = 0, cv = 1;
-    if (sscanf(o, "%d,%d,%d", &b, &q, &cv) >= 1) {
-      int ncu = 0;
-      (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device);
-      const int per = ncu / split_xcds(ncu);
-      if (q <= 0) q = per - b;
-      if (b > 0 && q > 0 && b + q <= per) {
-        c->split_b = b;
-        c->split_q = q;
-        c->split_curv = cv ? 1 : 0;
-      }
-    }
-  }
   if (stream) {
     c->stream = (hipStream_t)stream;
   } else {
@@ -2261,35 +2195,8 @@ void navgpu_destroy(navgpu_ctx *ctx) {
   }
   if (ctx->ev_fork) (void)hipEventDestroy(ctx->ev_fork);
   if (ctx->ev_join) (void)hipEventDestroy(ctx->ev_join);
-  if (ctx->ev_built) (void)hipEventDestroy(ctx->ev_built);
-  if (ctx->ev_curv) (void)hipEventDestroy(ctx->ev_curv);
-  // the split streams are shared by the process's contexts: kept
   if (ctx->own_stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;
-}
-
-int navgpu_set_cu_split(navgpu_ctx *ctx, int build_cus, int query_cus, int curv_on_query) {
-  ARG_CHECK(ctx && build_cus >= 0 && query_cus >= 0);
-  int ncu = 0;
-  HIP_TRY(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, ctx->device));
-  const int per = ncu / split_xcds(ncu);
-  if (build_cus == 0) {
-    HIP_TRY(hipStreamSynchronize(ctx->stream));
-    ctx->split_b = ctx->split_q = 0;
-    ctx->sb = ctx->sq = nullptr;
-    return NAVGPU_OK;
-  }
-  if (query_cus == 0) query_cus = per - build_cus;
-  if (query_cus <= 0 || build_cus + query_cus > per) {
-    set_err("cu split %d + %d exceeds the %d CUs of an XCD", build_cus, query_cus, per);
-    return NAVGPU_ERANGE;
-  }
-  HIP_TRY(hipStreamSynchronize(ctx->stream));
-  ctx->split_b = build_cus;
-  ctx->split_q = query_cus;
-  ctx->split_curv = curv_on_query ? 1 : 0;
-  ctx->sb = ctx->sq = nullptr;
-  return ensure_split(ctx);
 }
 
 int navgpu_set_stream(navgpu_ctx *ctx, void *stream) {

@@ -169,13 +169,6 @@ struct navgpu_ctx {
   double knn_lambda = 22.0;  // expected targets inside a query's first filter radius
   bool knn_stats = false;
   int screen_rows = 0, screen_S = 0;  // last screened rows_match call (tie diagnostic)
-  // CU split of the global-mode pair path (navgpu_set_cu_split): the index
-  // build on `split_b` CUs of every XCD (stream sb), the query pass on the
-  // next `split_q` (stream sq); both streams are shared by every context of
-  // the process with the same split. split_curv: curvature on sb (0) or sq (1)
-  int split_b = 0, split_q = 0, split_curv = 1;
-  hipStream_t sb = nullptr, sq = nullptr;
-  hipEvent_t ev_built = nullptr, ev_curv = nullptr;
 };
 
 namespace nv {
@@ -239,10 +232,6 @@ int knn_stamps_take(unsigned long long *out16);
 
 // side stream of a context, created on first use
 int ensure_aux(navgpu_ctx *ctx);
-
-// the CU-masked build / query streams of ctx's split (split_b > 0), created
-// on first use (process-wide per device and split), and ctx's events
-int ensure_split(navgpu_ctx *ctx);
 
 // R1 curvature of up to two clouds (both R x C, row-major Points) in one
 // launch on `stream` (src/slam.c:11-61); navgpu.hip

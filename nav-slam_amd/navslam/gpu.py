@@ -59,7 +59,6 @@ def _declare(L):
         "navgpu_knn_host": (C.c_int, [_vp, _vp, _sz, _vp, _sz, C.c_int, _vp, _vp]),
         "navgpu_pair_knn_dev": (C.c_int, [_vp, _vp, _vp, C.c_int, C.c_int, C.c_int,
                                           _vp, _vp, _vp, _vp]),
-        "navgpu_set_cu_split": (C.c_int, [_vp, C.c_int, C.c_int, C.c_int]),
         "navgpu_kd_build_dev": (C.c_int, [_vp, _vp, _sz, C.c_int]),
         "navgpu_kd_build_host": (C.c_int, [_vp, _vp, _sz, C.c_int]),
         "navgpu_malloc": (C.c_int, [_vp, _sz, C.POINTER(_vp)]),
@@ -157,12 +156,6 @@ class NavGpu:
 
     def sync(self):
         self._check(self.L.navgpu_sync(self.h), "sync")
-
-    def set_cu_split(self, build_cus, query_cus=0, curv_on_query=True):
-        """Global-mode build on `build_cus` CUs of every XCD, query on the
-        next `query_cus` (0 = the rest); build_cus = 0 turns it off."""
-        self._check(self.L.navgpu_set_cu_split(self.h, build_cus, query_cus,
-                                               1 if curv_on_query else 0), "set_cu_split")
 
     @property
     def rows_max_cols(self):
