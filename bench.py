@@ -84,7 +84,9 @@ def parse():
                    help="comma-separated rocprofv3 --pmc counter_collection.csv files "
                         "(FETCH_SIZE and WRITE_SIZE passes) to derive HBM bytes")
     p.add_argument("--traffic-json", default=None,
-                   help="per-step HBM bytes measured by scripts/round_profile.sh (PMC passes)")
+                   help="per-step HBM bytes from the PMC passes (scripts/round_evidence.sh "
+                        "writes them via scripts/traffic_json.py; default "
+                        "profiles/traffic_<workload>.json)")
     p.add_argument("--no-traffic-json", action="store_true")
     p.add_argument("--no-stream-copy", action="store_true",
                    help="skip the STREAM-copy ceiling measurement")

@@ -56,6 +56,12 @@ struct __align__(16) PRec {
   double x, y, z;
   int idx, cx;
 };
+// the same point as k_knnw stages it (r4): the f32 offset from the f64
+// centre of its cell, o + (c + 0.5) e per axis, and the cell's x index
+struct __align__(16) SRec {
+  float x, y, z;
+  int cx;
+};
 
 // ---- k_knn tile geometry (LDS budget: 4 blocks of 192 threads per CU)
 #ifndef NAVGPU_KNN_TILE_THREADS
@@ -339,15 +345,38 @@ struct BinPt {
   double x, y, z;
   int idx, cell;
 };
+// a query's coarse-bucketed key (k_bin_scatter -> k_bin_fine)
+struct QKey {
+  int cell, idx;
+};
 struct BinSide {
   const double *p;
   int n, P, nblk;
   int tab;  // offset of this side's table in the concatenated table
   int *start;
-  BinPt *bin;    // coarse-bucketed points
+  BinPt *bin;    // targets: coarse-bucketed points
+  QKey *key;     // queries: coarse-bucketed (cell, index) keys
   PRec *sorted;  // targets: cell-sorted records
-  int *perm;     // queries: cell-sorted position -> bucketed position
+  SRec *srec;    // targets: the same, as k_knnw stages them
+  int *perm;     // queries: cell-sorted position -> the caller's index
+  int *qcell;    // queries: cell-sorted position -> cell
 };
+// the queries as the query passes read them: the caller's cloud, through the
+// cell-sorted permutation
+struct QSide {
+  const double *pts;
+  const int *idx, *cell;
+};
+__device__ __forceinline__ BinPt qload(const QSide &QS, int pos) {
+  BinPt Q;
+  Q.idx = QS.idx[pos];
+  Q.cell = QS.cell[pos];
+  const double *p = QS.pts + 3 * (size_t)Q.idx;
+  Q.x = p[0];
+  Q.y = p[1];
+  Q.z = p[2];
+  return Q;
+}
 struct BinJob {
   BinSide s[2];
   int shift, nb;  // buckets per side
@@ -435,13 +464,17 @@ __global__ __launch_bounds__(256) void k_bin_scatter(BinJob J, const GridParams 
   __syncthreads();
   bin_chunk(S, blk, G, [&](int i, const P3 &v, int c) {
     const int pos = atomicAdd(&cur[c >> J.shift], 1);
-    BinPt t;
-    t.x = v.x;
-    t.y = v.y;
-    t.z = v.z;
-    t.idx = i;
-    t.cell = c;
-    S.bin[pos] = t;
+    if (side) {
+      S.key[pos] = QKey{c, i};
+    } else {
+      BinPt t;
+      t.x = v.x;
+      t.y = v.y;
+      t.z = v.z;
+      t.idx = i;
+      t.cell = c;
+      S.bin[pos] = t;
+    }
   });
 }
 
@@ -477,6 +510,7 @@ __global__ __launch_bounds__(kBinFineThreads) void k_bin_fine(BinJob J,
   const int n = hi - lo;
   const bool staged = side && n <= qstage;
   const BinPt *src = S.bin;
+  const QKey *qk = S.key;
   const int bd = (int)blockDim.x, tid = (int)threadIdx.x;
   for (int j = tid; j < ncell; j += bd) cnt[j] = 0;
   __syncthreads();
@@ -488,7 +522,7 @@ __global__ __launch_bounds__(kBinFineThreads) void k_bin_fine(BinJob J,
 #pragma unroll
     for (int u = 0; u < kFineStageHold; ++u) {
       const int sl = u * bd + tid;
-      if (sl < n) scell[u] = src[lo + sl].cell;
+      if (sl < n) scell[u] = qk[lo + sl].cell;
     }
 #pragma unroll
     for (int u = 0; u < kFineStageHold; ++u)
@@ -498,10 +532,13 @@ __global__ __launch_bounds__(kBinFineThreads) void k_bin_fine(BinJob J,
     for (int u = 0; u < kBinFineHold; ++u) {
       const int i = lo + u * bd + tid;
       if (i < held_end) {
-        if (side)
-          hold[u].cell = src[i].cell;
-        else
+        if (side) {
+          const QKey e = qk[i];
+          hold[u].cell = e.cell;
+          hold[u].idx = e.idx;
+        } else {
           hold[u] = src[i];
+        }
       }
     }
 #pragma unroll
@@ -509,7 +546,8 @@ __global__ __launch_bounds__(kBinFineThreads) void k_bin_fine(BinJob J,
       const int i = lo + u * bd + tid;
       if (i < held_end) atomicAdd(&cnt[hold[u].cell - base], 1);
     }
-    for (int i = held_end + tid; i < hi; i += bd) atomicAdd(&cnt[src[i].cell - base], 1);
+    for (int i = held_end + tid; i < hi; i += bd)
+      atomicAdd(&cnt[(side ? qk[i].cell : src[i].cell) - base], 1);
   }
   __syncthreads();
   // exclusive scan over the bucket's cells: each thread owns a contiguous run
@@ -526,7 +564,8 @@ __global__ __launch_bounds__(kBinFineThreads) void k_bin_fine(BinJob J,
     acc += v;
   }
   __syncthreads();
-  const int g0 = gp->g[0];
+  const GridParams &G = *gp;
+  const int g0 = G.g[0], g1 = G.g[1];
   if (staged) {
 #pragma unroll
     for (int u = 0; u < kFineStageHold; ++u) {
@@ -534,21 +573,36 @@ __global__ __launch_bounds__(kBinFineThreads) void k_bin_fine(BinJob J,
       if (sl < n) lslot[atomicAdd(&cnt[scell[u] - base], 1) - lo] = (uint16_t)sl;
     }
     __syncthreads();
-    for (int j = tid; j < n; j += bd) S.perm[lo + j] = lo + lslot[j];
+    for (int j = tid; j < n; j += bd) {
+      const QKey e = qk[lo + lslot[j]];
+      S.perm[lo + j] = e.idx;
+      S.qcell[lo + j] = e.cell;
+    }
     return;
   }
   auto place = [&](const BinPt &e, int i) {
     const int pos = atomicAdd(&cnt[e.cell - base], 1);
     if (side) {
-      S.perm[pos] = i;
+      S.perm[pos] = e.idx;
+      S.qcell[pos] = e.cell;
     } else {
       PRec t;
       t.x = e.x;
       t.y = e.y;
       t.z = e.z;
       t.idx = e.idx;
-      t.cx = e.cell % g0;
+      const int row = e.cell / g0;
+      t.cx = e.cell - row * g0;
       S.sorted[pos] = t;
+      // offsets from the f64 cell centre (k_knnw adds the centre's shift
+      // into its frame: DESIGN.md §4, SRec)
+      const int cy = row % g1, cz = row / g1;
+      SRec r;
+      r.x = (float)(e.x - (G.o[0] + (t.cx + 0.5) * G.e[0]));
+      r.y = (float)(e.y - (G.o[1] + (cy + 0.5) * G.e[1]));
+      r.z = (float)(e.z - (G.o[2] + (cz + 0.5) * G.e[2]));
+      r.cx = t.cx;
+      S.srec[pos] = r;
     }
   };
 #pragma unroll
@@ -556,7 +610,16 @@ __global__ __launch_bounds__(kBinFineThreads) void k_bin_fine(BinJob J,
     const int i = lo + u * bd + tid;
     if (i < held_end) place(hold[u], i);
   }
-  for (int i = held_end + tid; i < hi; i += bd) place(src[i], i);
+  for (int i = held_end + tid; i < hi; i += bd) {
+    if (side) {
+      BinPt e;
+      e.cell = qk[i].cell;
+      e.idx = qk[i].idx;
+      place(e, i);
+    } else {
+      place(src[i], i);
+    }
+  }
 }
 
 // ============================================================ k-NN helpers
@@ -703,7 +766,7 @@ template <int K>
 __global__ __launch_bounds__(kTileThreads, kKnnMinWaves) void k_knn(
     const GridParams *__restrict__ gp, const int *__restrict__ tstart,
     const PRec *__restrict__ tsort, const int *__restrict__ qstart,
-    const BinPt *__restrict__ qbin, const int *__restrict__ qperm, int32_t *__restrict__ oidx,
+    const QSide QS, int32_t *__restrict__ oidx,
     double *__restrict__ odist, KnnLists L_, float lambda) {
   __shared__ __attribute__((aligned(16))) float spair[2 * kZgOff];
   // cbr[r][j]: the LDS slot of the record at cell-sorted position g of cell
@@ -850,7 +913,7 @@ __global__ __launch_bounds__(kTileThreads, kKnnMinWaves) void k_knn(
       const int q0 = qstart[cell0 + qa], q1 = qstart[cell0 + qb + 1];
       for (int qi = q0 + tid; qi < q1 && !(kAbl & kAblNoQuery); qi += kTileThreads) {
         NV_STAMP(ts0);
-        const BinPt Q = qbin[qperm[qi]];
+        const BinPt Q = qload(QS, qi);
         const double qv[3] = {Q.x, Q.y, Q.z};
         const int qcx = Q.cell - (z * G.g[1] + y) * G.g[0];  // the cell's x index
         const int c[3] = {qcx, y, z};
@@ -1110,6 +1173,553 @@ __global__ __launch_bounds__(kTileThreads, kKnnMinWaves) void k_knn(
   NV_ACC_FLUSH;
 }
 
+// ============================================================ k_knnw
+// The query pass in wave chunks (r4): one WAVE per chunk of 64 consecutive
+// cell-sorted queries, no block barriers. k_knn's tiles were W query cells of
+// one grid row on a 3-wave block: ~146 queries on 192 lanes (0.77 of the
+// lanes), every tile paying stage -> barrier -> scan -> barrier. Here a chunk
+// is exactly 64 queries wherever the grid rows break; its queries fall into a
+// few SEGMENTS (one per grid row they touch, 1-2 on uniform data) and the
+// wave stages every segment's 9 neighbouring row pieces into its own LDS
+// region, column-major as in k_knn: segment s owns virtual columns
+// [vc0_s, vc0_s + ncol_s), its cells xf_s - S .. xl_s + S, each column the
+// records of its 9 (y, z) rows in turn, so a query's block is still ONE
+// contiguous slot range. Each segment has its own f32 frame (the tile centre
+// of k_knn for the segment's query cells). A chunk whose segments need more
+// than kWCols columns or kWRec records is done in rounds over a prefix of its
+// lanes; a lane whose block alone exceeds kWRec goes to k_knn_slow.
+// The per-query scan, exact stage and certificate are k_knn's.
+#ifndef NAVGPU_KNNW_REC
+#define NAVGPU_KNNW_REC 800
+#endif
+#ifndef NAVGPU_KNNW_MINW
+#define NAVGPU_KNNW_MINW 3
+#endif
+constexpr int kWRec = NAVGPU_KNNW_REC;   // staged records per wave (16 B each)
+constexpr int kWPairs = kWRec / 2 + 2;   // two spare pairs: read-ahead
+constexpr int kWZg = 4 * kWPairs;        // floats from the XY plane to the ZG plane
+constexpr int kWCols = 2 * kWave;        // staged columns per round: two per lane
+constexpr int kWSegs = 8;                // segments (grid rows) per round
+#ifndef NAVGPU_KNNW_U
+#define NAVGPU_KNNW_U 1
+#endif
+
+// inclusive wave64 prefix sum by DPP (row_shr 1/2/4/8, row_bcast 15/31):
+// every lane must be active
+__device__ __forceinline__ int wave_scan_add(int x) {
+  x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xf, 0xf, false);
+  x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xf, 0xf, false);
+  x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xf, 0xf, false);
+  x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xf, 0xf, false);
+  x += __builtin_amdgcn_update_dpp(0, x, 0x142, 0xa, 0xf, false);
+  x += __builtin_amdgcn_update_dpp(0, x, 0x143, 0xc, 0xf, false);
+  return x;
+}
+
+__device__ __forceinline__ int rdlane(int v, int l) { return __builtin_amdgcn_readlane(v, l); }
+
+// the f32 frame of a segment whose query cells are xf .. xl of row (y, z):
+// k_knn's tile centre; Dt bounds every staged offset (cell slack included)
+struct WFrame {
+  double o[3], Dt;
+};
+__device__ __forceinline__ WFrame wframe(const GridParams &G, int xf, int xl, int y, int z) {
+  WFrame F;
+  F.o[0] = G.o[0] + (xf + 0.5 * (xl - xf + 1)) * G.e[0];
+  F.o[1] = G.o[1] + (y + 0.5) * G.h;
+  F.o[2] = G.o[2] + (z + 0.5) * G.h;
+  F.Dt = G.clamped ? G.emax + 2.0 * G.h
+                   : fmax((0.5 * (xl - xf + 1) + G.sx + 1) * G.e[0], 2.0 * G.h) + 4.0 * G.delta;
+  return F;
+}
+
+#ifdef NAVGPU_STAMPS
+// k_knnw's phase stamps: one record per chunk, written by lane 0 (atomics on
+// shared slots from every wave would serialise at the memory side and
+// distort what they time); knn_stamps_take sums them
+constexpr int kWStampChunks = 1 << 15;
+__device__ unsigned long long g_wstamps[kWStampChunks][8];
+#define NV_WFLUSH(chunk)                                             \
+  if (threadIdx.x == 0 && (chunk) < kWStampChunks) {                 \
+    _Pragma("unroll") for (int s_ = 1; s_ < 9; ++s_)                 \
+      g_wstamps[chunk][s_ - 1] = nv_acc[s_];                         \
+  }
+#else
+#define NV_WFLUSH(chunk)
+#endif
+
+template <int K>
+__global__ __launch_bounds__(kWave, NAVGPU_KNNW_MINW) void k_knnw(const GridParams *__restrict__ gp,
+                                                   const int *__restrict__ tstart,
+                                                   const PRec *__restrict__ tsort,
+                                                   const SRec *__restrict__ srec,
+                                                   const QSide QS, int nq, int ntg,
+                                                   int32_t *__restrict__ oidx,
+                                                   double *__restrict__ odist, KnnLists L_) {
+  __shared__ __attribute__((aligned(16))) float spair[2 * kWZg];
+  __shared__ int colst[kWCols + 1];  // first slot of virtual column v; [kWCols] = total
+  // each segment's 9 row pieces: [sbnd[s][r][0], sbnd[s][r][1])
+  __shared__ int sbnd[kWSegs][9][2];
+  constexpr int KL = K + 1;
+  static_assert(K >= 1 && K <= 16, "K");
+  const GridParams G = *gp;
+  const int S = G.sx;
+  const int g0 = G.g[0], g1 = G.g[1], g2 = G.g[2];
+  // chunks dealt to the 8 XCDs in contiguous ranges (block b -> XCD b % 8)
+  const int nchunk = (nq + kWave - 1) / kWave;
+  const int per = (nchunk + 7) / 8;
+  const int chunk = (int)(blockIdx.x & 7) * per + (int)(blockIdx.x >> 3);
+  if (chunk >= nchunk) return;
+  const int lane = (int)threadIdx.x;
+  NV_ACC_DECL;
+  NV_STAMP(w0);
+  const int nlive = min(kWave, nq - chunk * kWave);
+  const int qi = chunk * kWave + lane;
+  const bool live = lane < nlive;
+  BinPt Q;
+#ifdef NAVGPU_KNNW_CHECK
+  if (live && (QS.idx[qi] < 0 || QS.idx[qi] >= nq || QS.cell[qi] < 0)) {
+    printf("knnw chunk %d lane %d: query %d idx %d cell %d\n", chunk, lane, qi, QS.idx[qi],
+           QS.cell[qi]);
+    return;
+  }
+#endif
+  if (live) Q = qload(QS, qi);
+  // the query's cell: x, row = (z g1 + y); rows ascend over the lanes
+  const int qrow = live ? Q.cell / g0 : 0x7fffffff;
+  const int qx = live ? Q.cell - qrow * g0 : 0;
+  const int qy = live ? qrow % g1 : 0, qz = live ? qrow / g1 : 0;
+  const uint32_t vmask = ~kKeyMask;
+  // rows ascend over the live lanes: a lane starts (ends) a grid row when the
+  // lane before (after) it holds another one (the shuffles run on every lane:
+  // a lane masked off by a short-circuit would hand its neighbour garbage)
+  const int prow = __shfl_up(qrow, 1, kWave), nrow = __shfl_down(qrow, 1, kWave);
+  const unsigned long long rowfirst = __ballot(live && (lane == 0 || prow != qrow));
+  const unsigned long long rowlast = __ballot(live && (lane == nlive - 1 || nrow != qrow));
+  NV_STAMP(w1);
+  NV_ACC(1, w0, w1);
+  for (int la = 0; la < nlive;) {
+    NV_STAMP(r0);
+    NV_ACC(7, 0ull, 1ull);
+    // ---- segments of lanes [la, nlive): a grid row each (the first one may
+    // start mid-row after a cut round)
+    const bool in = lane >= la && live;
+    const unsigned long long fall = rowfirst & (~0ull << la) | (1ull << la);
+    const unsigned long long below = (2ull << lane) - 1;  // lanes <= lane (lane 63: all)
+    const int sf = 63 - __builtin_clzll(fall & below | 1ull);  // the lane's segment: first lane
+    const int sl = (int)__builtin_ctzll(rowlast & ~(below >> 1) | (1ull << 63));  // ... last
+    const bool first = in && sf == lane, last = in && sl == lane;
+    const int xf = __shfl(qx, sf, kWave);  // the segment's first query cell
+    const int colq = qx - xf + S;          // the lane's cell: column in its segment
+    const int val = last ? colq + S + 1 : 0;  // columns of a segment, at its last lane
+    const int incv = wave_scan_add(val);
+    const int pre = in ? incv - val : 0;   // columns of earlier segments
+    const int vcq = pre + colq;            // the lane's cell: virtual column
+    const int cum = vcq + S + 1;           // columns if the round ended here
+    // the round: the lane prefix whose columns fit (cum ascends over the
+    // lanes) in at most kWSegs segments
+    const int segi = __popcll(fall & below) - 1;
+    int lb = la + __popcll(__ballot(in && cum <= kWCols && segi < kWSegs));
+    const int lbc = lb;  // the frames use the column-fit round (a budget cut keeps them)
+    int NC = rdlane(cum, lb - 1);
+    unsigned long long fb = __ballot(first && lane < lb);  // segment starts
+    // ---- column tables: virtual column v = lane + 64 p -> cell (vx, vy, vz);
+    // cs = its records (the 9 rows'), cbr[p][r] + g = the slot of the record
+    // at cell-sorted position g of row r; dxc = the column's cell centre in
+    // its segment's frame (x)
+    int cbr[2][9], st[2][9], en[2][9];
+    float dxc[2];
+    int total;
+    {
+      int cs[2], vx[2], vy[2], vz[2];
+      double fox[2];
+#pragma unroll
+      for (int p = 0; p < 2; ++p) {
+        vx[p] = vy[p] = vz[p] = 0;
+        cs[p] = 0;
+        fox[p] = 0.0;
+      }
+      for (unsigned long long b = fb; b; b &= b - 1) {
+        const int f = (int)__builtin_ctzll(b);
+        const int f_vc0 = rdlane(pre, f), f_xf = rdlane(qx, f), f_x0 = f_xf - S;
+        const int f_y = rdlane(qy, f), f_z = rdlane(qz, f);
+        const int f_xl = rdlane(qx, min(rdlane(sl, f), lbc - 1));
+        const double f_ox = wframe(G, f_xf, f_xl, f_y, f_z).o[0];
+#pragma unroll
+        for (int p = 0; p < 2; ++p) {
+          const int v = lane + kWave * p;
+          if (v >= f_vc0) {
+            vx[p] = f_x0 + (v - f_vc0);
+            vy[p] = f_y;
+            vz[p] = f_z;
+            fox[p] = f_ox;
+          }
+        }
+      }
+      const int np = NC > kWave ? 2 : 1;
+#pragma unroll
+      for (int p = 0; p < 2; ++p) {
+        const int v = lane + kWave * p;
+        // the f64 cell centre k_bin_fine measured the SRec offsets from
+        dxc[p] = (float)((G.o[0] + (vx[p] + 0.5) * G.e[0]) - fox[p]);
+#pragma unroll
+        for (int r = 0; r < 9; ++r) {
+          st[p][r] = en[p][r] = 0;
+          const int yy = vy[p] + (r % 3) - 1, zz = vz[p] + (r / 3) - 1;
+          if (p < np && v < NC && yy >= 0 && yy < g1 && zz >= 0 && zz < g2) {
+            const int base = (zz * g1 + yy) * g0;
+            st[p][r] = tstart[base + min(max(vx[p], 0), g0)];
+            en[p][r] = tstart[base + min(max(vx[p] + 1, 0), g0)];
+          }
+        }
+#pragma unroll
+        for (int r = 0; r < 9; ++r) cs[p] += en[p][r] - st[p][r];
+      }
+      const int inc0 = wave_scan_add(cs[0]);
+      const int tot0 = rdlane(inc0, kWave - 1);
+      const int inc1 = np > 1 ? wave_scan_add(cs[1]) + tot0 : tot0;
+      total = rdlane(inc1, kWave - 1);
+      const int ex[2] = {inc0 - cs[0], inc1 - cs[1]};
+#pragma unroll
+      for (int p = 0; p < 2; ++p) {
+        int a = ex[p];
+#pragma unroll
+        for (int r = 0; r < 9; ++r) {
+          cbr[p][r] = a - st[p][r];
+          a += en[p][r] - st[p][r];
+        }
+        colst[lane + kWave * p] = ex[p];
+      }
+      if (lane == 0) colst[kWCols] = total;
+    }
+    wave_sync_mem();
+    NV_STAMP(r1);
+    NV_ACC(2, r0, r1);
+    if (total > kWRec) {
+      // the lane prefix whose blocks end within the budget (slot ends ascend)
+      const bool inr = in && lane < lb;
+      const int endslot = inr ? colst[vcq + S + 1] : 0x7fffffff;
+      const int lb2 = la + __popcll(__ballot(inr && endslot <= kWRec));
+      if (lb2 == la) {
+        // the first lane's block alone exceeds the budget: it and every lane
+        // of its cell go to k_knn_slow from an infinite bound
+        const int vq0 = rdlane(vcq, la);
+        const bool same = inr && vcq == vq0;
+        if (same) {
+          push_slow(L_, qi, INFINITY);
+          atomicAdd(L_.n_unstaged, 1);
+        }
+        la += __popcll(__ballot(same));
+        wave_sync_mem();  // colst is rewritten by the next round
+        continue;
+      }
+      lb = lb2;
+      NC = rdlane(cum, lb - 1);
+      fb &= lb >= kWave ? ~0ull : ((1ull << lb) - 1);
+    }
+    const bool two = NC > kWave;
+    // ---- each segment's row pieces: the starts at its first column, the
+    // ends at its last (the round's cut included), from the tables
+    {
+      int si = 0;
+      for (unsigned long long b = fb; b; b &= b - 1, ++si) {
+        const int f = (int)__builtin_ctzll(b);
+        const int lsl = min(rdlane(sl, f), lb - 1);
+        const int vc0 = rdlane(pre, f), vlast = rdlane(cum, lsl) - 1;
+#pragma unroll
+        for (int p = 0; p < 2; ++p) {
+          const int v = lane + kWave * p;
+#pragma unroll
+          for (int r = 0; r < 9; ++r) {
+            if (v == vc0) sbnd[si][r][0] = st[p][r];
+            if (v == vlast) sbnd[si][r][1] = en[p][r];
+          }
+        }
+      }
+    }
+    wave_sync_mem();
+#ifdef NAVGPU_KNNW_CHECK
+    for (int q = lane; q < kWRec; q += kWave) spair[kWZg + (q >> 1) * 4 + 2 + (q & 1)] = __int_as_float(-1);
+    wave_sync_mem();
+#endif
+    // ---- staging: per segment, its 9 row pieces as SRec (16 B: f32 offset
+    // from the record's cell centre + x cell); every load of a segment in
+    // flight before any is used; slot from cbr, x shift from dxc (the
+    // record's column's lane), y and z shifts per row
+    int si = 0;
+    for (unsigned long long b = fb; b; b &= b - 1, ++si) {
+      const int f = (int)__builtin_ctzll(b);
+      const int lsl = min(rdlane(sl, f), lb - 1);
+      const int vc0 = rdlane(pre, f), vlast = rdlane(cum, lsl) - 1;
+      const int sxf = rdlane(qx, f), sy = rdlane(qy, f), sz = rdlane(qz, f);
+      const WFrame F = wframe(G, sxf, rdlane(qx, min(rdlane(sl, f), lbc - 1)), sy, sz);
+      const int x0 = sxf - S;
+      const int tlast = max(ntg - 1, 0);  // (srec holds at least one record)
+      constexpr int U = NAVGPU_KNNW_U;
+      int glo[9], nr[9];
+#pragma unroll
+      for (int r = 0; r < 9; ++r) {
+        glo[r] = sbnd[si][r][0];
+        nr[r] = sbnd[si][r][1] - glo[r];
+      }
+      for (int k0 = 0;; k0 += U * kWave) {
+        SRec v[9][U];
+        bool more = false;
+        // every load is issued, unconditionally, from a position clamped into
+        // the cloud (a per-element condition makes hipcc branch around each
+        // load and wait for it: nine serial round trips); lanes past a row
+        // piece discard theirs below. (The clamp also keeps a logic error
+        // from reading past the cloud, which would fault the device.)
+#pragma unroll
+        for (int r = 0; r < 9; ++r)
+#pragma unroll
+          for (int u = 0; u < U; ++u) {
+            const int k = k0 + u * kWave + lane;
+#ifdef NAVGPU_KNNW_CHECK
+            if (k < nr[r] && (glo[r] + k < 0 || glo[r] + k >= ntg))
+              printf("knnw chunk %d lane %d seg %d row %d: srec %d of %d (glo %d nr %d)\n", chunk,
+                     lane, si, r, glo[r] + k, ntg, glo[r], nr[r]);
+#endif
+            v[r][u] = srec[min(max(glo[r] + k, 0), tlast)];
+          }
+#pragma unroll
+        for (int r = 0; r < 9; ++r) {
+          more |= k0 + U * kWave < nr[r];
+          const int yy = sy + (r % 3) - 1, zz = sz + (r / 3) - 1;
+          const float dy = (float)((G.o[1] + (yy + 0.5) * G.e[1]) - F.o[1]);
+          const float dz = (float)((G.o[2] + (zz + 0.5) * G.e[2]) - F.o[2]);
+#pragma unroll
+          for (int u = 0; u < U; ++u) {
+            const int k = k0 + u * kWave + lane;
+            const int vcol = vc0 + v[r][u].cx - x0;
+            const int il = vcol & (kWave - 1);
+            int cb = __shfl(cbr[0][r], il, kWave);
+            float dx = __shfl(dxc[0], il, kWave);
+            if (two) {  // wave-uniform
+              const int c1 = __shfl(cbr[1][r], il, kWave);
+              const float d1 = __shfl(dxc[1], il, kWave);
+              cb = vcol >= kWave ? c1 : cb;
+              dx = vcol >= kWave ? d1 : dx;
+            }
+            if (k < nr[r] && vcol <= vlast) {
+              const int slot = cb + glo[r] + k;
+              float *d = spair + (slot >> 1) * 4 + (slot & 1);
+              d[0] = v[r][u].x + dx;
+              d[2] = v[r][u].y + dy;
+              d[kWZg] = v[r][u].z + dz;
+              d[kWZg + 2] = __int_as_float(glo[r] + k);
+            }
+          }
+        }
+        if (!more) break;  // wave-uniform: nr and k0 are
+      }
+    }
+    wave_sync_mem();
+    NV_STAMP(r2);
+    NV_ACC(3, r1, r2);
+    // the last query cell of the lane's segment in the column-fit round (its frame)
+    const int xl = __shfl(qx, min(sl, lbc - 1), kWave);
+#ifdef NAVGPU_KNNW_CHECK
+    if (in && lane < lb) {
+      const int t0 = colst[vcq - S], t1 = colst[vcq + S + 1];
+      int bad = -1;
+      for (int q = t0; q < t1; ++q)
+        if (__float_as_int(spair[kWZg + (q >> 1) * 4 + 2 + (q & 1)]) < 0) bad = q;
+      if (bad >= 0) {
+        printf("CHK chunk %d lane %d la %d lb %d lbc %d NC %d total %d vcq %d sf %d sl %d t0 %d t1 %d bad %d fb %llx qx %d qrow %d\n",
+               chunk, lane, la, lb, lbc, NC, total, vcq, sf, sl, t0, t1, bad, fb, qx, qrow);
+        for (int v = vcq - S; v <= vcq + S + 1; ++v) printf("CHK chunk %d colst[%d] = %d\n", chunk, v, colst[v]);
+      }
+    }
+    {
+      int si2 = 0;
+      for (unsigned long long b = fb; b; b &= b - 1, ++si2) {
+        const int f = (int)__builtin_ctzll(b);
+        const int lsl = min(rdlane(sl, f), lb - 1);
+        if (lane == 0 && (chunk == 5 || chunk == 36 || chunk == 40))
+          printf("SEG chunk %d si %d f %d lsl %d vc0 %d vlast %d x %d..%d row %d | %d %d %d %d %d %d %d %d %d / %d %d %d %d %d %d %d %d %d\n",
+                 chunk, si2, f, lsl, rdlane(pre, f), rdlane(cum, lsl) - 1, rdlane(qx, f), rdlane(qx, lsl), rdlane(qrow, f),
+                 sbnd[si2][0][0], sbnd[si2][1][0], sbnd[si2][2][0], sbnd[si2][3][0], sbnd[si2][4][0], sbnd[si2][5][0], sbnd[si2][6][0], sbnd[si2][7][0], sbnd[si2][8][0],
+                 sbnd[si2][0][1], sbnd[si2][1][1], sbnd[si2][2][1], sbnd[si2][3][1], sbnd[si2][4][1], sbnd[si2][5][1], sbnd[si2][6][1], sbnd[si2][7][1], sbnd[si2][8][1]);
+      }
+    }
+#endif
+    // ---- the round's queries, one per lane (k_knn's scan, exact stage and
+    // certificate on the lane's block [t0, t1))
+    if (in && lane < lb) {
+      const double qv[3] = {Q.x, Q.y, Q.z};
+      const int c[3] = {qx, qy, qz};
+      const int t0 = colst[vcq - S], t1 = colst[vcq + S + 1];
+      const WFrame F = wframe(G, xf, xl, qy, qz);
+      const double qr[3] = {qv[0] - F.o[0], qv[1] - F.o[1], qv[2] - F.o[2]};
+      const double Dq = fmax(F.Dt, fmax(fabs(qr[0]), fmax(fabs(qr[1]), fabs(qr[2]))));
+      // each f32 difference is within dl of the exact one: the staged target
+      // offset s + d carries <= 4 u Dq (s from the cell centre, the centre's
+      // shift d, their sum), the query's u Dq, the subtraction 2 u Dq, with
+      // u = 2^-24 (SRec)
+      const double dl = Dq * 0x1p-21;
+      const f2 qx2 = {(float)qr[0], (float)qr[0]}, qy2 = {(float)qr[1], (float)qr[1]},
+               qz2 = {(float)qr[2], (float)qr[2]};
+      const double Lr = block_reach(G, qv, c, 1);
+      uint32_t key[KL];
+#pragma unroll
+      for (int s = 0; s < KL; ++s) key[s] = kNoKey;
+      auto ins = [&](uint32_t kk) {  // keep the K+1 smallest keys sorted
+#pragma unroll
+        for (int s = K; s > 0; --s) key[s] = umed3(key[s - 1], key[s], kk);
+        key[0] = min(key[0], kk);
+      };
+      auto dist2 = [&](const float *p) {  // packed f32 squared distances of a pair
+        const float4 xy = *(const float4 *)p;
+        const float2 zz = *(const float2 *)(p + kWZg);
+        const f2 fx2 = f2{xy.x, xy.y} - qx2, fy2 = f2{xy.z, xy.w} - qy2,
+                 fz2 = f2{zz.x, zz.y} - qz2;
+        return __builtin_elementwise_fma(fz2, fz2, __builtin_elementwise_fma(fy2, fy2, fx2 * fx2));
+      };
+      const int ta = t0 & ~1;
+      const int npr = (t1 - ta + 1) >> 1;  // pairs the block touches
+      const bool overflow = (t1 - ta) > (1 << kKeyBits);
+      const float *cur = spair + (ta >> 1) * 4;
+      if (npr > 0) {  // first pair: may start before the block (odd t0) or end past it
+        const f2 d = dist2(cur);
+        const uint32_t k0 = knn_key(d[0], vmask, 0u), k1 = knn_key(d[1], vmask, 1u);
+        if (ta >= t0) ins(k0);
+        if (ta + 1 < t1) ins(k1);
+        cur += 4;
+      }
+      if (npr > 2) {  // interior pairs: the key's local id is the wave-uniform pair counter
+        const float *lastp = spair + ((ta >> 1) + npr - 1) * 4;
+        uint32_t v2 = 2;
+        float4 xy = *(const float4 *)cur;
+        float2 zz = *(const float2 *)(cur + kWZg);
+        do {
+          const float4 nxy = *(const float4 *)(cur + 4);
+          const float2 nzz = *(const float2 *)(cur + 4 + kWZg);
+          const f2 fx2 = f2{xy.x, xy.y} - qx2, fy2 = f2{xy.z, xy.w} - qy2,
+                   fz2 = f2{zz.x, zz.y} - qz2;
+          const f2 d =
+              __builtin_elementwise_fma(fz2, fz2, __builtin_elementwise_fma(fy2, fy2, fx2 * fx2));
+          ins(knn_key(d[0], vmask, v2));
+          ins(knn_key(d[1], vmask, v2 + 1));
+          cur += 4;
+          v2 += 2;
+          xy = nxy;
+          zz = nzz;
+        } while (cur < lastp);
+      }
+      if (npr > 1) {  // last pair: may end past the block
+        const f2 d = dist2(cur);
+        const uint32_t lid = (uint32_t)(2 * (npr - 1)) & kKeyMask;
+        const uint32_t k0 = (__float_as_uint(d[0]) & vmask) | lid;
+        const uint32_t k1 = (__float_as_uint(d[1]) & vmask) | (lid + 1);
+        ins(k0);
+        if (ta + 2 * (npr - 1) + 1 < t1) ins(k1);
+      }
+      NV_STAMP(r3);
+      NV_ACC(4, r2, r3);
+      bool ok = !overflow && Dq < 1e17;
+      // exact f64 stage on the K best keys (as in k_knn)
+      double ed[K];
+      int ei[K];
+      if (key[0] != kNoKey) {
+        int gpos[K];
+#pragma unroll
+        for (int s = 0; s < K; ++s) {
+          const uint32_t kk = key[s] != kNoKey ? key[s] : key[0];
+          const int p = min(max(ta + (int)(kk & kKeyMask), t0), max(t1 - 1, t0));
+          gpos[s] = __float_as_int(spair[kWZg + (p >> 1) * 4 + 2 + (p & 1)]);
+        }
+#pragma unroll
+        for (int s = 0; s < K; ++s) {
+          const bool val = key[s] != kNoKey;
+          gpos[s] = min(max(gpos[s], 0), max(ntg - 1, 0));  // (as the staging clamp above)
+#ifdef NAVGPU_KNNW_CHECK
+          if (gpos[s] < 0 || gpos[s] >= ntg) {
+            printf("knnw chunk %d lane %d: gpos %d of %d (key %x t0 %d t1 %d)\n", chunk, lane,
+                   gpos[s], ntg, key[s], t0, t1);
+            gpos[s] = 0;
+          }
+#endif
+          const PRec *tp = tsort + gpos[s];
+          const double2 xy = *(const double2 *)&tp->x;
+          const double2 zi = *(const double2 *)&tp->z;
+          const double pz = zi.x;
+          const int pid = __double2loint(zi.y);
+          const double ddx = xy.x - qv[0], ddy = xy.y - qv[1], ddz = pz - qv[2];
+          const double dsq = ddx * ddx + ddy * ddy + ddz * ddz;  // utils/kdtree.c:16
+          ei[s] = val ? pid : -1;
+          ed[s] = val ? __builtin_sqrt(dsq) : INFINITY;
+          if (val && !(ed[s] < INFINITY)) {  // an inf/NaN distance is never a neighbour (kdtree.c:117)
+            ed[s] = INFINITY;
+            ei[s] = -1;
+            ok = false;
+          }
+        }
+      } else {
+#pragma unroll
+        for (int s = 0; s < K; ++s) {
+          ed[s] = INFINITY;
+          ei[s] = -1;
+        }
+      }
+      // certificate bound on every candidate left out
+      double B = INFINITY;
+      if (Lr < INFINITY) {
+        const double Lg = Lr - 2.0 * G.delta;
+        B = Lg > 0.0 ? Lg * Lg : 0.0;
+      }
+      if (key[K] != kNoKey) {
+        const double V = (double)__uint_as_float(key[K] & vmask);
+        B = fmin(B, V - f32_err(V, dl));
+      }
+      bool sorted = true;
+#pragma unroll
+      for (int s = 1; s < K; ++s) sorted &= !knn_less_bf(ed[s], ei[s], ed[s - 1], ei[s - 1]);
+      for (int pass = 0; pass < K - 1 && __any(!sorted); ++pass) {
+#pragma unroll
+        for (int u = 1; u < K; ++u) knn_cx(ed[u - 1], ei[u - 1], ed[u], ei[u]);
+        sorted = true;
+#pragma unroll
+        for (int s = 1; s < K; ++s) sorted &= !knn_less_bf(ed[s], ei[s], ed[s - 1], ei[s - 1]);
+      }
+      const double dk = ed[K - 1];
+      const double dk2 = dk * dk;
+      if (dk < INFINITY)
+        ok = ok && B > dk2 * (1.0 + 0x1p-46);
+      else
+        ok = ok && B == INFINITY;
+      if (ok) {
+        const size_t q = (size_t)Q.idx;
+        if (K % 4 == 0 && L_.vec_out) {
+#pragma unroll
+          for (int s = 0; s < K; s += 4)
+            *(int4 *)(oidx + q * K + s) = make_int4(ei[s], ei[s + 1], ei[s + 2], ei[s + 3]);
+#pragma unroll
+          for (int s = 0; s < K; s += 2)
+            *(double2 *)(odist + q * K + s) = make_double2(ed[s], ed[s + 1]);
+        } else {
+#pragma unroll
+          for (int s = 0; s < K; ++s) {
+            oidx[q * K + s] = ei[s];
+            odist[q * K + s] = ed[s];
+          }
+        }
+      } else {
+        push_slow(L_, qi, (dk < INFINITY && !overflow) ? dk2 * (1.0 + 0x1p-46) : INFINITY);
+      }
+      NV_STAMP(r4);
+      NV_ACC(5, r3, r4);
+    }
+    NV_STAMP(r5);
+    NV_ACC(6, r2, r5);
+    la = lb;
+    wave_sync_mem();  // LDS is restaged by the next round
+  }
+  NV_STAMP(w9);
+  NV_ACC(8, w0, w9);
+  NV_WFLUSH(chunk);
+}
+
 // ============================================================ k_knn_slow
 // insert (d, id) into the sorted exact list kd/ki if it ranks among the K
 template <int K>
@@ -1189,8 +1799,7 @@ template <int K>
 __global__ __launch_bounds__(256) void k_knn_slow(const GridParams *__restrict__ gp,
                                                   const int *__restrict__ start,
                                                   const PRec *__restrict__ tsort,
-                                                  const BinPt *__restrict__ qbin,
-                                                  const int *__restrict__ qperm,
+                                                  const QSide QS,
                                                   int32_t *__restrict__ oidx,
                                                   double *__restrict__ odist, KnnLists L_) {
   __shared__ double sd[4][kWave];  // per-wave survivor buffers (256 threads)
@@ -1202,7 +1811,7 @@ __global__ __launch_bounds__(256) void k_knn_slow(const GridParams *__restrict__
   const int nwaves = (int)(gridDim.x * blockDim.x / kWave);
   const int gmax = max((G.g[0] + G.sx - 1) / G.sx, max(G.g[1], G.g[2]));
   for (int e = wave; e < n; e += nwaves) {
-    const BinPt Q = qbin[qperm[L_.slow_q[e]]];
+    const BinPt Q = qload(QS, L_.slow_q[e]);
     const size_t q = (size_t)Q.idx;
     double thr = L_.slow_thr[e];
     const double qv[3] = {Q.x, Q.y, Q.z};
@@ -1363,6 +1972,12 @@ int knn_stamps_take(unsigned long long *out16) {
   HIP_TRY(hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_stamps), 16 * 8));
   unsigned long long z[16] = {0};
   HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), z, 16 * 8));
+  // k_knnw's per-chunk records, summed into slots 1..8 (zeroed after)
+  std::vector<unsigned long long> w((size_t)kWStampChunks * 8);
+  HIP_TRY(hipMemcpyFromSymbol(w.data(), HIP_SYMBOL(g_wstamps), w.size() * 8));
+  for (size_t i = 0; i < w.size(); ++i) out16[1 + i % 8] += w[i];
+  std::fill(w.begin(), w.end(), 0ull);
+  HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_wstamps), w.data(), w.size() * 8));
   return NAVGPU_OK;
 #else
   (void)out16;
@@ -1415,8 +2030,11 @@ static int knn_run(navgpu_ctx *ctx, const double *tgt, size_t nt, const double *
   double *part;
   GridParams *gp;
   int *tab, *tstart, *qstart, *bbase, *counters;
-  BinPt *tbin = nullptr, *qbin;
+  BinPt *tbin = nullptr;
+  QKey *qkey;
+  int *qcell;
   PRec *tsort = nullptr;
+  SRec *srec = nullptr;
   int *qperm;
   RC(ws(ctx, kBBox, (size_t)kBBoxBlocks * 6, &part));
   RC(ws(ctx, kParams, 1, &gp));
@@ -1427,19 +2045,26 @@ static int knn_run(navgpu_ctx *ctx, const double *tgt, size_t nt, const double *
   RC(ws(ctx, kBSum, 2 * (size_t)J.nb, &btot));
   RC(ws(ctx, kCellId, 2 * ((size_t)J.nb + 1), &bbase));
   RC(ws(ctx, kStats, 4, &counters));  // zeroed by k_grid_params
-  if (nt) {
-    RC(ws(ctx, kSlotBuf, nt, &tbin));
-    RC(ws(ctx, kTSort, nt, &tsort));
-  }
-  RC(ws(ctx, kQCell, nq, &qbin));
+  if (nt) RC(ws(ctx, kSlotBuf, nt, &tbin));
+  // at least one record each: k_knnw loads from clamped positions unconditionally
+  RC(ws(ctx, kTSort, std::max<size_t>(nt, 1), &tsort));
+  RC(ws(ctx, kSRec, std::max<size_t>(nt, 1), &srec));
+  RC(ws(ctx, kQCell, nq, &qkey));
   RC(ws(ctx, kQPerm, nq, &qperm));
+  RC(ws(ctx, kQSort, nq, &qcell));
   J.s[0].p = tgt;
   J.s[1].p = queries;
   J.s[0].start = tstart;
   J.s[1].start = qstart;
   J.s[0].bin = tbin;
-  J.s[1].bin = qbin;
+  J.s[1].bin = nullptr;
+  J.s[0].key = nullptr;
+  J.s[1].key = qkey;
+  J.s[0].qcell = nullptr;
+  J.s[1].qcell = qcell;
   J.s[0].sorted = tsort;
+  J.s[0].srec = srec;
+  J.s[1].srec = nullptr;
   J.s[1].sorted = nullptr;
   J.s[0].perm = nullptr;
   J.s[1].perm = qperm;
@@ -1489,11 +2114,21 @@ static int knn_run(navgpu_ctx *ctx, const double *tgt, size_t nt, const double *
   const dim3 g(8 * nbx), b(kTileThreads);
   const dim3 gs(std::max<unsigned>(1, std::min<unsigned>(2048, grid1d(nq, 256))));
   const float lambda = (float)ctx->knn_lambda;
+  // k_knnw: one 64-lane block per chunk of 64 cell-sorted queries, chunks
+  // dealt to the XCDs in contiguous ranges
+  const int nchunk = (int)((nq + kWave - 1) / kWave);
+  const dim3 gw(8 * ((nchunk + 7) / 8)), bw(kWave);
+  const bool waves = ctx->knn_mode == 1;
+  const QSide QS{queries, qperm, qcell};
 #define KNN_CASE(KK)                                                                        \
   case KK:                                                                                  \
-    hipLaunchKernelGGL((k_knn<KK>), g, b, 0, s, gp, tstart, tsort, qstart, qbin, qperm, idx,  \
-                       dist, lists, lambda);                                                \
-    hipLaunchKernelGGL((k_knn_slow<KK>), gs, dim3(256), 0, s, gp, tstart, tsort, qbin, qperm, \
+    if (waves)                                                                              \
+      hipLaunchKernelGGL((k_knnw<KK>), gw, bw, 0, s, gp, tstart, tsort, srec, QS, (int)nq, (int)nt, \
+                         idx, dist, lists);                                                 \
+    else                                                                                    \
+      hipLaunchKernelGGL((k_knn<KK>), g, b, 0, s, gp, tstart, tsort, qstart, QS,   \
+                         idx, dist, lists, lambda);                                         \
+    hipLaunchKernelGGL((k_knn_slow<KK>), gs, dim3(256), 0, s, gp, tstart, tsort, QS,       \
                        idx, dist, lists);                                                   \
     break;
   switch (k) {

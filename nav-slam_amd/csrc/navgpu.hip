@@ -2150,6 +2150,7 @@ int navgpu_create(int device, void *stream, navgpu_ctx **out) {
   c->device = device;
   if (const char *st = getenv("NAVGPU_KNN_STATS")) c->knn_stats = *st && *st != '0';
   if (const char *o = getenv("NAVGPU_KNN_BLOCKS")) c->knn_blocks = atoi(o);
+  if (const char *o = getenv("NAVGPU_KNN_MODE")) c->knn_mode = atoi(o) == 0 ? 0 : 1;
   if (const char *o = getenv("NAVGPU_KNN_SX")) {
     const int v = atoi(o);
     if (v >= 1 && v <= kKnnMaxSx) c->knn_sx = v;
@@ -2849,7 +2850,11 @@ int navgpu_kd_build_dev(navgpu_ctx *ctx, double *pts, size_t n, int depth0) {
       hipLaunchKernelGGL(k_sel_scatter, grid, dim3(kSelThreads), 0, ctx->stream, st, P, Ptmp, T);
       hipLaunchKernelGGL(k_sel_update, dim3(1), dim3(256), 0, ctx->stream, st, kRounds);
       CHECK_LAUNCH("k_sel");
-      if ((long long)it > 4LL * ni + 64) {  // quickselect shrinks its window every iteration
+      // every iteration places its pivot, so a window of at most maxlen + 1
+      // positions is done within maxlen + 1 iterations: a level still active
+      // past that is stuck (a logic error), and fails at once instead of
+      // spinning through 4 n iterations
+      if ((long long)it > (long long)maxlen + 64) {
         set_err("kd_build: selection did not converge (level %d)", d);
         return NAVGPU_EHIP;
       }

@@ -49,6 +49,7 @@ if hasattr(g.L, "navgpu_debug_stamps") and g.L.navgpu_debug_stamps(st) == 0:
     names = ["-", "tile_setup+stage", "tile_queries", "q_scan", "q_exact", "n_q_waves", "n_tiles",
              "tile_barrier"]
     stamps = {names[i]: int(st[i]) for i in range(1, 8)}
+    stamps["raw"] = [int(st[i]) for i in range(16)]
 b_ms, bn = g.timing_read("knn_build")
 print(json.dumps({"lib": os.path.basename(a.lib or "libnavgpu.so"), "occ": float(a.occ), "k": a.k, "query_us": 1000 * q_ms / qn,
                   "build_us": 1000 * b_ms / bn, "slow_lanes": slow,
