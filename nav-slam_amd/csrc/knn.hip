@@ -1284,7 +1284,7 @@ __global__ __launch_bounds__(kWave, NAVGPU_KNNW_MINW) void k_knnw(const GridPara
     return;
   }
 #endif
-  if (live) Q = qload(QS, qi);
+  Q = qload(QS, min(qi, nq - 1));  // (unconditional: see the table loads)
   // the query's cell: x, row = (z g1 + y); rows ascend over the lanes
   const int qrow = live ? Q.cell / g0 : 0x7fffffff;
   const int qx = live ? Q.cell - qrow * g0 : 0;
@@ -1362,15 +1362,27 @@ __global__ __launch_bounds__(kWave, NAVGPU_KNNW_MINW) void k_knnw(const GridPara
         const int v = lane + kWave * p;
         // the f64 cell centre k_bin_fine measured the SRec offsets from
         dxc[p] = (float)((G.o[0] + (vx[p] + 0.5) * G.e[0]) - fox[p]);
+        if (p < np) {  // wave-uniform
+          // every load issued unconditionally (cells off the grid read
+          // tstart[0] and are zeroed after): a per-element condition makes
+          // hipcc branch around each load and wait for it
+          bool ok[9];
 #pragma unroll
-        for (int r = 0; r < 9; ++r) {
-          st[p][r] = en[p][r] = 0;
-          const int yy = vy[p] + (r % 3) - 1, zz = vz[p] + (r / 3) - 1;
-          if (p < np && v < NC && yy >= 0 && yy < g1 && zz >= 0 && zz < g2) {
-            const int base = (zz * g1 + yy) * g0;
-            st[p][r] = tstart[base + min(max(vx[p], 0), g0)];
-            en[p][r] = tstart[base + min(max(vx[p] + 1, 0), g0)];
+          for (int r = 0; r < 9; ++r) {
+            const int yy = vy[p] + (r % 3) - 1, zz = vz[p] + (r / 3) - 1;
+            ok[r] = v < NC && yy >= 0 && yy < g1 && zz >= 0 && zz < g2;
+            const int base = ok[r] ? (zz * g1 + yy) * g0 : 0;
+            st[p][r] = tstart[ok[r] ? base + min(max(vx[p], 0), g0) : 0];
+            en[p][r] = tstart[ok[r] ? base + min(max(vx[p] + 1, 0), g0) : 0];
           }
+#pragma unroll
+          for (int r = 0; r < 9; ++r) {
+            st[p][r] = ok[r] ? st[p][r] : 0;
+            en[p][r] = ok[r] ? en[p][r] : 0;
+          }
+        } else {
+#pragma unroll
+          for (int r = 0; r < 9; ++r) st[p][r] = en[p][r] = 0;
         }
 #pragma unroll
         for (int r = 0; r < 9; ++r) cs[p] += en[p][r] - st[p][r];
@@ -1417,7 +1429,6 @@ __global__ __launch_bounds__(kWave, NAVGPU_KNNW_MINW) void k_knnw(const GridPara
       NC = rdlane(cum, lb - 1);
       fb &= lb >= kWave ? ~0ull : ((1ull << lb) - 1);
     }
-    const bool two = NC > kWave;
     // ---- each segment's row pieces: the starts at its first column, the
     // ends at its last (the round's cut included), from the tables
     {
@@ -1445,75 +1456,84 @@ __global__ __launch_bounds__(kWave, NAVGPU_KNNW_MINW) void k_knnw(const GridPara
     // ---- staging: per segment, its 9 row pieces as SRec (16 B: f32 offset
     // from the record's cell centre + x cell); every load of a segment in
     // flight before any is used; slot from cbr, x shift from dxc (the
-    // record's column's lane), y and z shifts per row
-    int si = 0;
-    for (unsigned long long b = fb; b; b &= b - 1, ++si) {
-      const int f = (int)__builtin_ctzll(b);
-      const int lsl = min(rdlane(sl, f), lb - 1);
-      const int vc0 = rdlane(pre, f), vlast = rdlane(cum, lsl) - 1;
-      const int sxf = rdlane(qx, f), sy = rdlane(qy, f), sz = rdlane(qz, f);
-      const WFrame F = wframe(G, sxf, rdlane(qx, min(rdlane(sl, f), lbc - 1)), sy, sz);
-      const int x0 = sxf - S;
-      const int tlast = max(ntg - 1, 0);  // (srec holds at least one record)
-      constexpr int U = NAVGPU_KNNW_U;
-      int glo[9], nr[9];
+    // record's column's lane), y and z shifts per row. TWO: the round has
+    // columns past 64 (the second table of each lane), a separate copy so
+    // the usual one-table round shuffles only once per value.
+    auto stage = [&](auto TWO) {
+      int si = 0;
+      for (unsigned long long b = fb; b; b &= b - 1, ++si) {
+        const int f = (int)__builtin_ctzll(b);
+        const int lsl = min(rdlane(sl, f), lb - 1);
+        const int vc0 = rdlane(pre, f), vlast = rdlane(cum, lsl) - 1;
+        const int sxf = rdlane(qx, f), sy = rdlane(qy, f), sz = rdlane(qz, f);
+        const WFrame F = wframe(G, sxf, rdlane(qx, min(rdlane(sl, f), lbc - 1)), sy, sz);
+        const int x0 = sxf - S;
+        const int tlast = max(ntg - 1, 0);  // (srec holds at least one record)
+        constexpr int U = NAVGPU_KNNW_U;
+        int glo[9], nr[9];
 #pragma unroll
-      for (int r = 0; r < 9; ++r) {
-        glo[r] = sbnd[si][r][0];
-        nr[r] = sbnd[si][r][1] - glo[r];
-      }
-      for (int k0 = 0;; k0 += U * kWave) {
-        SRec v[9][U];
-        bool more = false;
-        // every load is issued, unconditionally, from a position clamped into
-        // the cloud (a per-element condition makes hipcc branch around each
-        // load and wait for it: nine serial round trips); lanes past a row
-        // piece discard theirs below. (The clamp also keeps a logic error
-        // from reading past the cloud, which would fault the device.)
-#pragma unroll
-        for (int r = 0; r < 9; ++r)
-#pragma unroll
-          for (int u = 0; u < U; ++u) {
-            const int k = k0 + u * kWave + lane;
-#ifdef NAVGPU_KNNW_CHECK
-            if (k < nr[r] && (glo[r] + k < 0 || glo[r] + k >= ntg))
-              printf("knnw chunk %d lane %d seg %d row %d: srec %d of %d (glo %d nr %d)\n", chunk,
-                     lane, si, r, glo[r] + k, ntg, glo[r], nr[r]);
-#endif
-            v[r][u] = srec[min(max(glo[r] + k, 0), tlast)];
-          }
-#pragma unroll
-        for (int r = 0; r < 9; ++r) {
-          more |= k0 + U * kWave < nr[r];
-          const int yy = sy + (r % 3) - 1, zz = sz + (r / 3) - 1;
-          const float dy = (float)((G.o[1] + (yy + 0.5) * G.e[1]) - F.o[1]);
-          const float dz = (float)((G.o[2] + (zz + 0.5) * G.e[2]) - F.o[2]);
-#pragma unroll
-          for (int u = 0; u < U; ++u) {
-            const int k = k0 + u * kWave + lane;
-            const int vcol = vc0 + v[r][u].cx - x0;
-            const int il = vcol & (kWave - 1);
-            int cb = __shfl(cbr[0][r], il, kWave);
-            float dx = __shfl(dxc[0], il, kWave);
-            if (two) {  // wave-uniform
-              const int c1 = __shfl(cbr[1][r], il, kWave);
-              const float d1 = __shfl(dxc[1], il, kWave);
-              cb = vcol >= kWave ? c1 : cb;
-              dx = vcol >= kWave ? d1 : dx;
-            }
-            if (k < nr[r] && vcol <= vlast) {
-              const int slot = cb + glo[r] + k;
-              float *d = spair + (slot >> 1) * 4 + (slot & 1);
-              d[0] = v[r][u].x + dx;
-              d[2] = v[r][u].y + dy;
-              d[kWZg] = v[r][u].z + dz;
-              d[kWZg + 2] = __int_as_float(glo[r] + k);
-            }
-          }
+        for (int r = 0; r < 9; ++r) {  // wave-uniform: scalar registers
+          glo[r] = __builtin_amdgcn_readfirstlane(sbnd[si][r][0]);
+          nr[r] = __builtin_amdgcn_readfirstlane(sbnd[si][r][1]) - glo[r];
         }
-        if (!more) break;  // wave-uniform: nr and k0 are
+        for (int k0 = 0;; k0 += U * kWave) {
+          SRec v[9][U];
+          bool more = false;
+          // every load is issued, unconditionally, from a position clamped
+          // into the cloud (a per-element condition makes hipcc branch around
+          // each load and wait for it: nine serial round trips); lanes past a
+          // row piece discard theirs below. (The clamp also keeps a logic
+          // error from reading past the cloud, which would fault the device.)
+#pragma unroll
+          for (int r = 0; r < 9; ++r)
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+              const int k = k0 + u * kWave + lane;
+#ifdef NAVGPU_KNNW_CHECK
+              if (k < nr[r] && (glo[r] + k < 0 || glo[r] + k >= ntg))
+                printf("knnw chunk %d lane %d seg %d row %d: srec %d of %d (glo %d nr %d)\n",
+                       chunk, lane, si, r, glo[r] + k, ntg, glo[r], nr[r]);
+#endif
+              // (a wave-uniform row base and a 32-bit lane offset)
+              v[r][u] = (srec + glo[r])[min(k, tlast - glo[r])];
+            }
+#pragma unroll
+          for (int r = 0; r < 9; ++r) {
+            more |= k0 + U * kWave < nr[r];
+            const int yy = sy + (r % 3) - 1, zz = sz + (r / 3) - 1;
+            const float dy = (float)((G.o[1] + (yy + 0.5) * G.e[1]) - F.o[1]);
+            const float dz = (float)((G.o[2] + (zz + 0.5) * G.e[2]) - F.o[2]);
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+              const int k = k0 + u * kWave + lane;
+              const int vcol = vc0 + v[r][u].cx - x0;
+              const int il = vcol & (kWave - 1);
+              int cb = __shfl(cbr[0][r], il, kWave);
+              float dx = __shfl(dxc[0], il, kWave);
+              if constexpr (decltype(TWO)::value) {
+                const int c1 = __shfl(cbr[1][r], il, kWave);
+                const float d1 = __shfl(dxc[1], il, kWave);
+                cb = vcol >= kWave ? c1 : cb;
+                dx = vcol >= kWave ? d1 : dx;
+              }
+              if (k < nr[r] && vcol <= vlast) {
+                const int slot = cb + glo[r] + k;
+                float *d = spair + (slot >> 1) * 4 + (slot & 1);
+                d[0] = v[r][u].x + dx;
+                d[2] = v[r][u].y + dy;
+                d[kWZg] = v[r][u].z + dz;
+                d[kWZg + 2] = __int_as_float(glo[r] + k);
+              }
+            }
+          }
+          if (!more) break;  // wave-uniform: nr and k0 are
+        }
       }
-    }
+    };
+    if (NC > kWave)
+      stage(std::true_type{});
+    else
+      stage(std::false_type{});
     wave_sync_mem();
     NV_STAMP(r2);
     NV_ACC(3, r1, r2);
@@ -1629,20 +1649,26 @@ __global__ __launch_bounds__(kWave, NAVGPU_KNNW_MINW) void k_knnw(const GridPara
           const int p = min(max(ta + (int)(kk & kKeyMask), t0), max(t1 - 1, t0));
           gpos[s] = __float_as_int(spair[kWZg + (p >> 1) * 4 + 2 + (p & 1)]);
         }
+        // all 2 K gathers in flight before any is used (the scheduler would
+        // otherwise sink each pair to its use: a chain of round trips)
+        double2 gxy[K], gzi[K];
+#pragma unroll
+        for (int s = 0; s < K; ++s) {
+#ifdef NAVGPU_KNNW_CHECK
+          if (gpos[s] < 0 || gpos[s] >= ntg)
+            printf("knnw chunk %d lane %d: gpos %d of %d (key %x t0 %d t1 %d)\n", chunk, lane,
+                   gpos[s], ntg, key[s], t0, t1);
+#endif
+          gpos[s] = min(max(gpos[s], 0), max(ntg - 1, 0));  // (as the staging clamp above)
+          const PRec *tp = tsort + gpos[s];
+          gxy[s] = *(const double2 *)&tp->x;
+          gzi[s] = *(const double2 *)&tp->z;
+        }
+        __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int s = 0; s < K; ++s) {
           const bool val = key[s] != kNoKey;
-          gpos[s] = min(max(gpos[s], 0), max(ntg - 1, 0));  // (as the staging clamp above)
-#ifdef NAVGPU_KNNW_CHECK
-          if (gpos[s] < 0 || gpos[s] >= ntg) {
-            printf("knnw chunk %d lane %d: gpos %d of %d (key %x t0 %d t1 %d)\n", chunk, lane,
-                   gpos[s], ntg, key[s], t0, t1);
-            gpos[s] = 0;
-          }
-#endif
-          const PRec *tp = tsort + gpos[s];
-          const double2 xy = *(const double2 *)&tp->x;
-          const double2 zi = *(const double2 *)&tp->z;
+          const double2 xy = gxy[s], zi = gzi[s];
           const double pz = zi.x;
           const int pid = __double2loint(zi.y);
           const double ddx = xy.x - qv[0], ddy = xy.y - qv[1], ddz = pz - qv[2];
