@@ -158,9 +158,12 @@ def cpu_baseline_k3(src, tgt, k, reps):
     to 8x8). Two legs, each the median of `reps` after one warm-up:
       1 core    : as the reference runs (single-threaded);
       threads_N : OpenMP over the queries on N threads (the search only reads
-                  the tree; N = OMP_NUM_THREADS, 16 on the GPU box)
-                  and over rows for the curvature; the tree build is the
-                  reference's serial recursion.
+                  the tree) and over rows for the curvature; the tree build is
+                  the reference's serial recursion. N = OMP_NUM_THREADS: the
+                  GPU box allots 16 host CPUs to a one-GPU job (its harness
+                  sets OMP_NUM_THREADS=16 and asks jobs to keep within it);
+                  nproc counts the whole shared 8-GPU host (host_info), whose
+                  other CPUs belong to other jobs.
     """
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     from pyoracle import Oracle
@@ -199,7 +202,9 @@ def cpu_baseline_k3(src, tgt, k, reps):
                                    "cores": threads, "seconds_per_pair": round(tall, 4),
                                    "runs_s": [round(t, 4) for t in tsall],
                                    "note": "OpenMP over queries and curvature rows; serial "
-                                           "tree build"},
+                                           "tree build; N = OMP_NUM_THREADS, the host CPUs the "
+                                           "GPU box allots to a one-GPU job (nproc counts the "
+                                           "whole shared host)"},
             "host": host,
             "sample": (f"the full K3 pair 0 ({N} queries vs {N} targets), median of {reps} after "
                        "1 warm-up: extract_feature on both clouds + buildKDTree + "
@@ -243,7 +248,8 @@ def cpu_baseline_k2(src, tgt, reps):
                                    "cores": threads, "seconds_per_pair": round(tall, 5),
                                    "runs_s": [round(t, 5) for t in tsall],
                                    "note": "OpenMP over rows (build + queries) and curvature "
-                                           "rows"},
+                                           "rows; N = OMP_NUM_THREADS, the host CPUs the GPU box "
+                                           "allots to a one-GPU job"},
             "host": host_info(),
             "sample": (f"one {src.shape[0]}x{src.shape[1]} L9-shaped pair ({nq[0]} source-feature "
                        f"queries), median of {reps} after 1 warm-up: extract_feature x2 + per-row "

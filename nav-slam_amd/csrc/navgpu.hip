@@ -564,12 +564,7 @@ __device__ int row_stage_and_build(const double *feat_src, const double *coords,
       });
   NV_STAMP(rs1);
   NV_STAMP_ADD0(8, rs0, rs1);
-#ifdef NAVGPU_DBG_ROWS_NOBUILD  // timing-only ablation: identity "tree"
-  for (int i = threadIdx.x; i < n; i += blockDim.x) P[i] = (uint16_t)i;
-  __syncthreads();
-#else
   block_build_kdtree<uint16_t>(FC, NS, n, P, (uint16_t *)(smem + L.t), 0);
-#endif
   return n;
 }
 
@@ -751,13 +746,8 @@ __global__ __launch_bounds__(kRowsBlock) void k_rows_match(
     const int c = QL[i];
     int bpos;
     double bd;
-#ifdef NAVGPU_DBG_ROWS_NOQUERY  // timing-only ablation
-    bpos = n ? (int)(i % n) : -1;
-    bd = sraw[3 * c];
-#else
     kd_query(TX, TY, TZ, n, sraw[3 * c], sraw[3 * c + 1], sraw[3 * c + 2],
              stk + threadIdx.x, blockDim.x, &bpos, &bd);
-#endif
     nn_idx[rowoff + c] = bpos >= 0 ? pair_row0 + canon_col(TX, TY, TZ, T, n, bpos) : -1;
     nn_dist[rowoff + c] = bd;
   }

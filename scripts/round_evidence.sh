@@ -53,7 +53,7 @@ step bench_k3_inflight1 300 python3 bench.py --inflight 1 --no-cpu-baseline --tr
 step bench_k2 300 python3 bench.py --workload k2 --steps 10 --traffic-json "$OUT/traffic_k2.json" --json-out "$OUT/bench_k2.json"
 step bench_k2i 300 python3 bench.py --workload k2 --integer-mm --steps 10 --traffic-json "$OUT/traffic_k2i.json" --json-out "$OUT/bench_k2i.json"
 step bench_k4 400 python3 bench.py --workload k4 --steps 3 --warmup 1 --traffic-json "$OUT/traffic_k4.json" --json-out "$OUT/bench_k4.json"
-step bench_k4i 400 python3 bench.py --workload k4 --integer-mm --steps 3 --warmup 1 --no-cpu-baseline --traffic-json "$OUT/traffic_k4i.json" --json-out "$OUT/bench_k4i.json"
+step bench_k4i 400 python3 bench.py --workload k4 --integer-mm --steps 3 --warmup 1 --traffic-json "$OUT/traffic_k4i.json" --json-out "$OUT/bench_k4i.json"
 step bench_k5 400 python3 bench.py --workload k5 --steps 30 --warmup 2 --json-out "$OUT/bench_k5.json"
 step bench_k5_fast 400 python3 bench.py --workload k5 --k5-mode fast --steps 30 --warmup 2 --traffic-json "$OUT/traffic_k5f.json" --json-out "$OUT/bench_k5_fast.json"
 step trace_k5 400 rocprofv3 --kernel-trace --stats -d "$OUT/trace_k5" -o run --output-format csv -- python3 bench.py --workload k5 --k5-mode fast --steps 20 --warmup 2 --no-cpu-baseline --no-traffic-json

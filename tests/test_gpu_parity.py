@@ -202,13 +202,14 @@ def test_rows_match_batch_equals_per_pair(gpu, orc):
             _eq(x, y, f"pair {p} {name}")
 
 
-def test_rows_match_batch_k4_full_size(gpu):
+def test_rows_match_batch_k4_full_size(gpu, orc):
     """K4 at full size, as bench.py --workload k4 builds it: 256 pairs of
     128 x 2048 (8 distinct L9-shaped pairs, seeds 5..12, cycled; here pair 3
     of every 8 is integer-mm, L9's native format) in ONE batch launch of
     rows_match_batch_dev, every pair compared with the single-pair rows_match
-    of the same clouds (which the reference digests pin,
-    test_rows_match_k2_matches_reference_digest)."""
+    of the same clouds, and each of the 8 distinct single-pair results
+    compared with the oracle's rows_match (pinned to the reference by
+    test_oracle.py and the K2 digests)."""
     import torch
     from navslam.synth import l9_pair
     R, Cc, P, ND = 128, 2048, 256, 8
@@ -225,6 +226,9 @@ def test_rows_match_batch_k4_full_size(gpu):
     singles = [gpu.rows_match(a, b) for a, b in distinct]
     assert (singles[3][2] >= 0).sum() > 100000  # the integer-mm pair has work
     names = ("src_mask", "tgt_mask", "nn_idx", "nn_dist")
+    for d, (a, b) in enumerate(distinct):  # every distinct pair pinned to the oracle
+        for x, y, name in zip(singles[d], orc.rows_match(a, b), names):
+            _eq(x, y, f"distinct pair {d} (seed {d + 5}) {name} vs oracle")
     got_all = [t.cpu().numpy() for t in (sm, tm, idx, dist)]
     for p in range(P):
         for x, y, name in zip(got_all, singles[p % ND], names):

@@ -7,6 +7,14 @@ oracle/Makefile `asan` builds, under -fsanitize=address,undefined with
                        (nav-slam_amd/jansson/jansson_mini.c), on edge inputs:
                        empty / single-point / duplicate / NaN trees, rows
                        without features, k > n, hostile JSON;
+  * shim_asan_54x42    the drop-in shim's host half (nav-slam_amd/csrc/
+                       navslam_shim.c: KDNode slabs and registry, list
+                       download, exact and fast Adam tails, host trees on and
+                       off) over oracle/navgpu_cpu_stub.c, a host stand-in
+                       for libnavgpu: 130 frames through the 100-frame map
+                       ring, exact-mode poses bit-identical to the oracle's
+                       frame loop, plus buildKDTree / nearestNeighborSearch /
+                       freeKDTree on a point set and a caller-linked tree;
   * nav_slam_ref_8x8, nav_slam_l9_ref_8x8 (with /root/reference): the K1
                        reference programs, whose L5 JSON and L9 CSV readers
                        (src/main.c:13-128) run over our jansson subset, fed the
@@ -47,6 +55,13 @@ def test_oracle_and_jansson_under_asan_ubsan(built):
                        text=True, timeout=600)
     _clean(p)
     assert "asan_driver ok" in p.stdout
+
+
+def test_shim_host_code_under_asan_ubsan(built):
+    p = subprocess.run([os.path.join(built, "shim_asan_54x42")], env=ENV, capture_output=True,
+                       text=True, timeout=600)
+    _clean(p)
+    assert "shim_asan ok" in p.stdout
 
 
 def _exe(built, name):
