@@ -132,6 +132,27 @@ int navgpu_kd_query_rows_dev(navgpu_ctx *ctx, const double *tree_pts,
                              int32_t *nn_pos, double *nn_dist,
                              int32_t *mask_out);
 
+/* ---- R4 without R5, and R6 over such rows: trees only where ties need them
+ * navgpu_kd_compact_rows_dev: navgpu_kd_build_rows_dev without the
+ * permutation: tree_pts/tree_col row r = the feature points in column order
+ * (flattenPoints, src/slam.c:64-81), tree_n as there. navgpu_kd_query_rows_
+ * lazy_dev: navgpu_kd_query_rows_dev over such rows: a query's minimum is
+ * unique, or its duplicates bit-identical, except on a genuine distance tie
+ * (DESIGN.md §2), and only those rows then get the reference's tree, built
+ * in place (tree_pts/tree_col row r permuted as navgpu_kd_build_rows_dev
+ * would), with all their queries walked. nn_pos indexes the row as it is on
+ * return (column order for untied rows). For a caller that needs no host
+ * KDNode trees (the shim with NAVSLAM_HOST_TREES=0): the per-row Lomuto
+ * chain (utils/kdtree.c:20-82) runs only for tied rows. */
+int navgpu_kd_compact_rows_dev(navgpu_ctx *ctx, const double *feat_src,
+                               const double *coords, int R, int C,
+                               double *tree_pts, int32_t *tree_col,
+                               int32_t *tree_n, int32_t *mask_out);
+int navgpu_kd_query_rows_lazy_dev(navgpu_ctx *ctx, double *tree_pts, int32_t *tree_col,
+                                  const int32_t *tree_n, const double *feat_src,
+                                  const double *queries, int R, int C, int32_t *nn_pos,
+                                  double *nn_dist, int32_t *mask_out);
+
 /* ---- R7: correspondence dedup per row (src/slam.c:247-284) -------------
  * Over the output of navgpu_kd_query_rows: of the queries of row r whose
  * nearest points have equal coordinates, keep the first column at the

@@ -534,7 +534,7 @@ extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
 // On return the block is synchronised; returns n.
 __device__ int row_stage_and_build(const double *feat_src, const double *coords,
                                    int r, int C, const RowsLds &L,
-                                   int32_t *mask_out) {
+                                   int32_t *mask_out, bool build = true) {
   double *raw = (double *)(smem + L.raw);
   double *FC = (double *)(smem + L.fc);
   uint16_t *FCOL = (uint16_t *)(smem + L.fcol);
@@ -564,7 +564,12 @@ __device__ int row_stage_and_build(const double *feat_src, const double *coords,
       });
   NV_STAMP(rs1);
   NV_STAMP_ADD0(8, rs0, rs1);
-  block_build_kdtree<uint16_t>(FC, NS, n, P, (uint16_t *)(smem + L.t), 0);
+  if (build) {
+    block_build_kdtree<uint16_t>(FC, NS, n, P, (uint16_t *)(smem + L.t), 0);
+  } else {  // the compacted features in column order (flattenPoints) only
+    for (int i = threadIdx.x; i < n; i += blockDim.x) P[i] = (uint16_t)i;
+    __syncthreads();
+  }
   return n;
 }
 
@@ -981,6 +986,21 @@ __device__ int compact_cols(int c0, int c1, const int32_t *__restrict__ mask, Lo
 struct ScreenSet {
   const double *TX, *TY, *TZ, *BOX;
   int nch;
+  __device__ double3 at(int e) const { return double3{TX[e], TY[e], TZ[e]}; }
+};
+// The same set read from the caller's row (r4, k_rows_screen32 keeps only
+// f32 offsets in LDS): compacted position e -> column FCOL[e] of the row
+// tg[3 * C]; positions from n on (the last chunk's tail) are +inf.
+struct ScreenSetG {
+  const double *tg;
+  const uint16_t *FCOL;
+  const double *BOX;
+  int nch, n;
+  __device__ double3 at(int e) const {
+    const double *p = tg + 3 * (int)FCOL[min(e, max(n - 1, 0))];
+    const double x = p[0], y = p[1], z = p[2];
+    return e < n ? double3{x, y, z} : double3{INFINITY, INFINITY, INFINITY};
+  }
 };
 
 // lower bound of the computed dsq between any point of box bx and any query
@@ -998,9 +1018,8 @@ __device__ __forceinline__ double screen_box_lb(const double *bx, double qlx, do
 // Chunk boxes of TX/TY/TZ[0, n) (NaN coordinates left out: such a point's
 // distance is NaN and never taken); 64 / kScreenChunk chunks per wave per
 // pass. The caller synchronises before the boxes are read.
-template <int NT>
-__device__ void screen_boxes(const double *TX, const double *TY, const double *TZ,
-                             double *BOX, int n, int nch) {
+template <int NT, class Set>
+__device__ void screen_boxes(const Set &T, double *BOX, int n, int nch) {
   const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
   constexpr int NW = NT / kWave, CPW = kWave / kScreenChunk;
   static_assert(kWave % kScreenChunk == 0, "chunks tile a wave");
@@ -1008,7 +1027,8 @@ __device__ void screen_boxes(const double *TX, const double *TY, const double *T
     const int b = b0 + lane / kScreenChunk, e = b * kScreenChunk + lane % kScreenChunk;
     const bool in = b < nch && e < n;
     double lo[3], hi[3];
-    const double v[3] = {in ? TX[e] : NAN, in ? TY[e] : NAN, in ? TZ[e] : NAN};
+    const double3 p = T.at(in ? e : 0);
+    const double v[3] = {in ? p.x : NAN, in ? p.y : NAN, in ? p.z : NAN};
 #pragma unroll
     for (int a = 0; a < 3; ++a) {
       const bool ok = v[a] == v[a];
@@ -1043,7 +1063,8 @@ __device__ void screen_boxes(const double *TX, const double *TY, const double *T
 // tests the chunk's box against the box of the wave's queries and the
 // largest runner-up of its lanes, and only chunks that pass get the
 // per-query test and the scan.
-__device__ void screen_query(const ScreenSet &T, bool act, double qx, double qy, double qz,
+template <class Set>
+__device__ void screen_query(const Set &T, bool act, double qx, double qy, double qz,
                              int s0, int s1, double &d1, double &d2, int &j1,
                              double bound2 = INFINITY) {
   const int lane = threadIdx.x & (kWave - 1);
@@ -1053,7 +1074,8 @@ __device__ void screen_query(const ScreenSet &T, bool act, double qx, double qy,
 #pragma unroll 8
     for (int u = 0; u < kScreenChunk; ++u) {
       const int e = e0 + u;
-      const double dx = T.TX[e] - qx, dy = T.TY[e] - qy, dz = T.TZ[e] - qz;
+      const double3 p = T.at(e);
+      const double dx = p.x - qx, dy = p.y - qy, dz = p.z - qz;
       const double d = dx * dx + dy * dy + dz * dz;  // utils/kdtree.c:16
       j1 = d < d1 ? e : j1;
       d2 = fmin(d2, fmax(d1, d));  // a NaN d makes d2 = d1: a (safe) tie
@@ -1097,7 +1119,8 @@ __device__ void screen_query(const ScreenSet &T, bool act, double qx, double qy,
 // (duplicated no-return points at the origin, integer data), so it is a
 // second pass over the chunks that can hold the band. Returns genuine (a
 // tie the tree must break) and emin, the lowest position of the duplicates.
-__device__ void screen_verify(const ScreenSet &T, bool act, double qx, double qy, double qz,
+template <class Set>
+__device__ void screen_verify(const Set &T, bool act, double qx, double qy, double qz,
                               double d1, double d2, int j1, bool &genuine, int &emin) {
   const double dist = __builtin_sqrt(d1);
   const bool suspect = act && d1 < INFINITY && __builtin_sqrt(d2) == dist;
@@ -1105,19 +1128,21 @@ __device__ void screen_verify(const ScreenSet &T, bool act, double qx, double qy
   emin = j1;
   if (!__any(suspect)) return;
   const int jr = j1 >= 0 ? j1 : 0;
-  const long long rx = __double_as_longlong(T.TX[jr]), ry = __double_as_longlong(T.TY[jr]),
-                  rz = __double_as_longlong(T.TZ[jr]);
+  const double3 pr = T.at(jr);
+  const long long rx = __double_as_longlong(pr.x), ry = __double_as_longlong(pr.y),
+                  rz = __double_as_longlong(pr.z);
   for (int k = 0; k < T.nch; ++k) {
     const double lb = screen_box_lb(T.BOX + 6 * k, qx, qx, qy, qy, qz, qz);
     if (!__any(suspect && __builtin_sqrt(lb) <= dist)) continue;
     for (int u = 0; u < kScreenChunk; ++u) {
       const int e = k * kScreenChunk + u;
-      const double dx = T.TX[e] - qx, dy = T.TY[e] - qy, dz = T.TZ[e] - qz;
+      const double3 p = T.at(e);
+      const double dx = p.x - qx, dy = p.y - qy, dz = p.z - qz;
       const double d = dx * dx + dy * dy + dz * dz;
       if (suspect && __builtin_sqrt(d) == dist) {
-        const bool same = __double_as_longlong(T.TX[e]) == rx &&
-                          __double_as_longlong(T.TY[e]) == ry &&
-                          __double_as_longlong(T.TZ[e]) == rz;
+        const bool same = __double_as_longlong(p.x) == rx &&
+                          __double_as_longlong(p.y) == ry &&
+                          __double_as_longlong(p.z) == rz;
         genuine |= !same;
         emin = same ? min(emin, e) : emin;
       }
@@ -1164,7 +1189,7 @@ __global__ __launch_bounds__(NT) void k_rows_screen(
   for (int e = n + (int)threadIdx.x; e < nch * kScreenChunk; e += NT)
     TX[e] = TY[e] = TZ[e] = INFINITY;
   const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
-  screen_boxes<NT>(TX, TY, TZ, BOX, n, nch);
+  screen_boxes<NT>(ScreenSet{TX, TY, TZ, BOX, nch}, BOX, n, nch);
   NV_STAMP(ss2);
   NV_STAMP_ADD(1, ss1, ss2);
   // this split's source features (block_compact synchronises, so the boxes
@@ -1219,15 +1244,229 @@ __global__ __launch_bounds__(NT) void k_rows_screen(
   if (threadIdx.x == 0) tie[(size_t)r * S + sp] = any;
 }
 
+// ---- k_rows_screen32 (r4): the screen's candidate scan in packed f32 -------
+// k_rows_screen's f64 scan issues ~12 VALU per candidate and the K4 batch is
+// VALU-bound. This kernel returns the same nn_idx / nn_dist /
+// tie flags from a packed-f32 scan with an f64 certificate:
+//  * LDS holds the row's target features as f32 offsets from the row's first
+//    feature o (12 B each instead of 24); the f64 points stay in the caller's
+//    row and are read through FCOL where an exact value is needed;
+//  * one query per lane keeps the two smallest keys, key = f32 dsq bits with
+//    the low kb bits replaced by the position (v_and_or + v_med3 + v_min per
+//    candidate; the distances two candidates per packed op);
+//  * certificate: the winner's reference dsq d1 is computed in f64. Every
+//    other candidate's f32 dsq is >= the runner-up key's truncated value, so
+//    when f32_bound(d1 (1 + 2^-40)) is below it, no other point is within
+//    sqrt-equality of d1: the answer is the unique argmin, which is what the
+//    f64 screen returns (no tie, no verify pass);
+//  * chunks are pruned by their exact f64 box bound against f32_upper of the
+//    runner-up key (>= the exact dsq of both key holders, so >= the final
+//    runner-up: a pruned point can neither win nor tie);
+//  * lanes without a certificate (near-ties within the key's 2^-(23-kb)
+//    resolution, duplicates, NaN / inf, coordinates beyond f32 range) run
+//    k_rows_screen's f64 screen + verify over the caller's row, pruned by that
+//    same runner-up bound.
+__host__ __device__ inline int rows_screen32_lds(int C, int w) {
+  const int cp = (C + kScreenChunk - 1) / kScreenChunk * kScreenChunk;
+  return 3 * align16(4 * cp) + 2 * align16(2 * C) + align16(48 * (cp / kScreenChunk)) +
+         align16(2 * w) + align16(4 * 160) + 16;
+}
+
+template <int NT>
+__global__ __launch_bounds__(NT) void k_rows_screen32(
+    const double *__restrict__ src, const double *__restrict__ tgt, int R, int C,
+    const int32_t *__restrict__ src_mask, const int32_t *__restrict__ tgt_mask,
+    int32_t *__restrict__ nn_idx, double *__restrict__ nn_dist, int32_t *__restrict__ tie) {
+  const int r = blockIdx.x, S = gridDim.y, sp = blockIdx.y;
+  const int w = (C + S - 1) / S;
+  const int c0 = sp * w, c1 = min(C, c0 + w);
+  const size_t rowoff = (size_t)r * C;
+  const int pair_row0 = (r % R) * C;
+  const int cp = (C + kScreenChunk - 1) / kScreenChunk * kScreenChunk;
+  float *XF = (float *)smem;
+  float *YF = (float *)(smem + align16(4 * cp));
+  float *ZF = (float *)(smem + 2 * align16(4 * cp));
+  uint16_t *FCOL = (uint16_t *)(smem + 3 * align16(4 * cp));
+  uint16_t *RANK = (uint16_t *)((unsigned char *)FCOL + align16(2 * C));
+  double *BOX = (double *)((unsigned char *)RANK + align16(2 * C));
+  uint16_t *QL = (uint16_t *)((unsigned char *)BOX + align16(48 * (cp / kScreenChunk)));
+  int *scan = (int *)((unsigned char *)QL + align16(2 * w));
+  unsigned *DT = (unsigned *)((unsigned char *)scan + align16(4 * 160));
+  const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
+  const double *tg = tgt + 3 * rowoff;
+  if (threadIdx.x == 0) *DT = 0u;
+  // target row features in column order (flattenPoints): positions only
+  const int n = compact_cols<NT>(
+      0, C, tgt_mask + rowoff, [&](int) { return 0; },
+      [&](int j, int pos, int) { FCOL[pos] = (uint16_t)j; }, RANK, scan);
+  const int nch = (n + kScreenChunk - 1) / kScreenChunk;
+  const ScreenSetG G = {tg, FCOL, BOX, nch, n};
+  const double3 o = n > 0 ? G.at(0) : double3{0.0, 0.0, 0.0};
+  // f32 offsets (the last chunk's tail +inf) and Dt >= every |t - o| (inf
+  // when some offset is not a finite f32: no lane of the row is certified)
+  float dtl = 0.0f;
+  for (int e = threadIdx.x; e < nch * kScreenChunk; e += NT) {
+    float fx = INFINITY, fy = INFINITY, fz = INFINITY;
+    if (e < n) {
+      const double3 p = G.at(e);
+      const double ex = p.x - o.x, ey = p.y - o.y, ez = p.z - o.z;
+      fx = (float)ex;
+      fy = (float)ey;
+      fz = (float)ez;
+      const double m = fmax(fabs(ex), fmax(fabs(ey), fabs(ez)));
+      dtl = m <= 1e37 ? fmaxf(dtl, (float)(m * (1.0 + 0x1p-20))) : INFINITY;
+      if (!(ex == ex && ey == ey && ez == ez)) dtl = INFINITY;
+    }
+    XF[e] = fx;
+    YF[e] = fy;
+    ZF[e] = fz;
+  }
+#pragma unroll
+  for (int off = kWave / 2; off > 0; off >>= 1) dtl = fmaxf(dtl, __shfl_xor(dtl, off, kWave));
+  if (lane == 0) atomicMax(DT, __float_as_uint(dtl));  // >= 0: the bits order as the values
+  screen_boxes<NT>(G, BOX, n, nch);
+  // this split's source features (compact_cols synchronises: offsets, boxes
+  // and Dt are visible after it)
+  const int32_t *sm = src_mask + rowoff;
+  const int nq = compact_cols<NT>(
+      c0, c1, sm, [&](int) { return 0; }, [&](int j, int pos, int) { QL[pos] = (uint16_t)j; },
+      nullptr, scan);
+  for (int j = c0 + (int)threadIdx.x; j < c1; j += NT)
+    if (!sm[j]) {
+      nn_idx[rowoff + j] = -1;
+      nn_dist[rowoff + j] = INFINITY;
+    }
+  const double Dt = (double)__uint_as_float(*DT);
+  // key: f32 dsq bits, the low kb bits the position (nch * 32 <= 2^kb)
+  const int kb = 32 - __builtin_clz((unsigned)max(nch * kScreenChunk - 1, 1));
+  const uint32_t idm = (1u << kb) - 1u, vmask = ~idm;
+  int mytie = 0;
+  for (int i0 = wid * kWave; i0 < nq; i0 += NT) {  // wave-uniform trip count
+    const int i = i0 + lane;
+    const bool act = i < nq;
+    const int c = QL[act ? i : i0];
+    const double *qp = src + 3 * (rowoff + c);
+    const double qx = qp[0], qy = qp[1], qz = qp[2];
+    // the chunks where the wave's columns start first (as k_rows_screen)
+    const int s0 = __builtin_amdgcn_readfirstlane(
+        min((int)RANK[QL[i0]] / kScreenChunk, max(nch - 1, 0)));
+    const int s1 = min(s0 + 1, max(nch - 1, 0));
+    const double rx = qx - o.x, ry = qy - o.y, rz = qz - o.z;
+    const double Dq = fmax(Dt, fmax(fabs(rx), fmax(fabs(ry), fabs(rz))));
+    // each f32 difference is within dl of the exact one: the target offset
+    // and the query offset are rounded once each (<= u D), the subtraction
+    // once (<= 2 u D), u = 2^-24
+    const double dl = Dq * 0x1p-21;
+    const f2 qx2 = {(float)rx, (float)rx}, qy2 = {(float)ry, (float)ry},
+             qz2 = {(float)rz, (float)rz};
+    uint32_t k1 = kNoKey32, k2 = kNoKey32;
+    auto scan32 = [&](int k) {
+      const int e0 = k * kScreenChunk;
+#pragma unroll
+      for (int u = 0; u < kScreenChunk; u += 2) {
+        const float2 xx = *(const float2 *)(XF + e0 + u);
+        const float2 yy = *(const float2 *)(YF + e0 + u);
+        const float2 zz = *(const float2 *)(ZF + e0 + u);
+        const f2 dx = f2{xx.x, xx.y} - qx2, dy = f2{yy.x, yy.y} - qy2, dz = f2{zz.x, zz.y} - qz2;
+        const f2 d = __builtin_elementwise_fma(dz, dz, __builtin_elementwise_fma(dy, dy, dx * dx));
+        const uint32_t a = knn_key(d[0], vmask, (uint32_t)(e0 + u));
+        const uint32_t b = knn_key(d[1], vmask, (uint32_t)(e0 + u + 1));
+        k2 = umed3(k1, k2, a);
+        k1 = min(k1, a);
+        k2 = umed3(k1, k2, b);
+        k1 = min(k1, b);
+      }
+    };
+    // upper bound of the exact dsq of both key holders (inf: no bound)
+    auto ub2 = [&]() {
+      const float V = __uint_as_float(k2 | idm);
+      return (V < INFINITY && dl < INFINITY) ? f32_upper((double)V, dl) : (double)INFINITY;
+    };
+    if (nch > 0) {
+      scan32(s0);
+      if (s1 != s0) scan32(s1);
+    }
+    const bool qok = act && qx == qx && qy == qy && qz == qz;
+    double wl[3] = {qok ? qx : INFINITY, qok ? qy : INFINITY, qok ? qz : INFINITY};
+    double wh[3] = {qok ? qx : -INFINITY, qok ? qy : -INFINITY, qok ? qz : -INFINITY};
+    double wd2 = qok ? ub2() : -INFINITY;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+#pragma unroll
+      for (int a = 0; a < 3; ++a) {
+        wl[a] = fmin(wl[a], __shfl_xor(wl[a], off, kWave));
+        wh[a] = fmax(wh[a], __shfl_xor(wh[a], off, kWave));
+      }
+      wd2 = fmax(wd2, __shfl_xor(wd2, off, kWave));
+    }
+    for (int k0 = 0; k0 < nch; k0 += kWave) {
+      const int kl = k0 + lane;
+      bool pass = false;
+      if (kl < nch && kl != s0 && kl != s1)
+        pass = screen_box_lb(BOX + 6 * kl, wl[0], wh[0], wl[1], wh[1], wl[2], wh[2]) <= wd2;
+      unsigned long long m = __ballot(pass);
+      while (m) {
+        const int k = k0 + __builtin_ctzll(m);
+        m &= m - 1;
+        const double lb = screen_box_lb(BOX + 6 * k, qx, qx, qy, qy, qz, qz);
+        if (__any(act && lb <= ub2())) scan32(k);
+      }
+    }
+    // the certificate (nch = 0: no candidate, nothing to certify)
+    int j1 = -1;
+    double d1 = INFINITY;
+    bool cert = nch == 0;
+    if (act && nch > 0) {
+      j1 = (int)(k1 & idm);
+      const double3 p = G.at(j1);
+      const double dx = p.x - qx, dy = p.y - qy, dz = p.z - qz;
+      d1 = dx * dx + dy * dy + dz * dz;  // utils/kdtree.c:16
+      const float lb2 = k2 == kNoKey32 ? INFINITY : __uint_as_float(k2 & vmask);
+      cert = d1 < INFINITY && Dq < 1e17 && f32_bound(d1 * (1.0 + 0x1p-40), dl) < lb2;
+    }
+    bool genuine = false;
+    int emin = j1;
+    const bool need = act && !cert;
+    if (__any(need)) {  // k_rows_screen's f64 path for these lanes
+      double f1 = INFINITY, f2v = INFINITY;
+      int fj = -1;
+      const double b2 = ub2();
+      screen_query(G, need, qx, qy, qz, nch > 0 ? s0 : -1, nch > 0 ? s1 : -1, f1, f2v, fj, b2);
+      bool gen;
+      int em;
+      screen_verify(G, need, qx, qy, qz, f1, f2v, fj, gen, em);
+      if (need) {
+        d1 = f1;
+        j1 = fj;
+        genuine = gen;
+        emin = em;
+      }
+    }
+    if (act) {
+      const double dist = __builtin_sqrt(d1);
+      const bool t = genuine || (d1 < INFINITY && dist > 0.0 && dist < 1e-150);
+      if (t) {
+        nn_idx[rowoff + c] = kTiePending;
+        mytie = 1;
+      } else {
+        nn_idx[rowoff + c] = j1 >= 0 ? pair_row0 + (int)FCOL[emin] : -1;
+        nn_dist[rowoff + c] = j1 >= 0 ? dist : INFINITY;
+      }
+    }
+  }
+  const int any = __syncthreads_or(mytie);
+  if (threadIdx.x == 0) tie[(size_t)r * S + sp] = any;
+}
+
 // ------------------------------------------- split per-row build / query
 __global__ __launch_bounds__(kRowsBuildBlock) void k_rows_build(
     const double *__restrict__ feat_src, const double *__restrict__ coords,
     int R, int C, double *__restrict__ tree_pts, int32_t *__restrict__ tree_col,
-    int32_t *__restrict__ tree_n, int32_t *__restrict__ mask_out) {
+    int32_t *__restrict__ tree_n, int32_t *__restrict__ mask_out, int build) {
   const RowsLds L = rows_lds(C, kRowsBlock, false);
   const int r = blockIdx.x;
   const size_t rowoff = (size_t)r * C;
-  const int n = row_stage_and_build(feat_src, coords, r, C, L, mask_out);
+  const int n = row_stage_and_build(feat_src, coords, r, C, L, mask_out, build != 0);
   const double *FC = (const double *)(smem + L.fc);
   const uint16_t *FCOL = (const uint16_t *)(smem + L.fcol);
   const uint16_t *P = (const uint16_t *)(smem + L.p);
@@ -1367,7 +1606,8 @@ template <int NT>
 __global__ __launch_bounds__(NT) void k_rows_query_screen(
     const double *__restrict__ tree_pts, const int32_t *__restrict__ tree_n,
     const double *__restrict__ feat_src, const double *__restrict__ queries, int R, int C,
-    int32_t *__restrict__ nn_pos, double *__restrict__ nn_dist, int32_t *__restrict__ mask_out) {
+    int32_t *__restrict__ nn_pos, double *__restrict__ nn_dist, int32_t *__restrict__ mask_out,
+    int32_t *__restrict__ tie) {
   const int r = blockIdx.x;
   const int w = (C + (int)gridDim.y - 1) / (int)gridDim.y;
   const int c0 = (int)blockIdx.y * w, c1 = min(C, c0 + w);
@@ -1398,7 +1638,7 @@ __global__ __launch_bounds__(NT) void k_rows_query_screen(
   const int lo = max(c0 - 2, 0), hi = min(c1 + 2, C);  // slice + curvature halo
   block_copy(rs, feat_src + 3 * (rowoff + lo), 3 * (hi - lo));
   __syncthreads();
-  screen_boxes<NT>(TX, TY, TZ, BOX, n, nch);
+  screen_boxes<NT>(ScreenSet{TX, TY, TZ, BOX, nch}, BOX, n, nch);
   for (int j = c0 + (int)threadIdx.x; j < c1; j += NT) {
     int f = 0;
     if (j >= 2 && j < C - 2) {  // src/slam.c:16 window
@@ -1465,11 +1705,103 @@ __global__ __launch_bounds__(NT) void k_rows_query_screen(
     if (act) {
       int bpos = j1 >= 0 ? emin : -1;
       double bd = j1 >= 0 ? dist : INFINITY;
-      if (genuine || (d1 < INFINITY && dist > 0.0 && dist < 1e-150))
-        kd_query(TX, TY, TZ, n, qx, qy, qz, stk + threadIdx.x, NT, &bpos, &bd);
+      if (genuine || (d1 < INFINITY && dist > 0.0 && dist < 1e-150)) {
+        if (tie)  // the row holds no tree yet: k_rows_retree walks all its queries
+          tie[r] = 1;
+        else
+          kd_query(TX, TY, TZ, n, qx, qy, qz, stk + threadIdx.x, NT, &bpos, &bd);
+      }
       nn_pos[rowoff + c] = bpos;
       nn_dist[rowoff + c] = bd;
     }
+  }
+}
+
+// K5 with the row trees left unbuilt (navgpu_kd_query_rows_lazy_dev): a row
+// whose screen found a genuine tie gets the reference's tree now, from the
+// compacted features that k_rows_build (build = 0) left in tree_pts in
+// column order (the array buildKDTree permutes, utils/kdtree.c:65-82), and
+// ALL its queries are answered by the walk (utils/kdtree.c:110-152), since
+// their positions now index the permuted row. Rows without a tie return.
+__global__ __launch_bounds__(kRowsBlock) void k_rows_retree(
+    double *__restrict__ tree_pts, int32_t *__restrict__ tree_col,
+    const int32_t *__restrict__ tree_n, const double *__restrict__ feat_src,
+    const double *__restrict__ queries, int C, int32_t *__restrict__ nn_pos,
+    double *__restrict__ nn_dist, const int32_t *__restrict__ tie) {
+  const int r = blockIdx.x;
+  if (!tie[r]) return;  // uniform
+  const RowsLds L = rows_lds(C, kRowsBlock, true);
+  const size_t rowoff = (size_t)r * C;
+  const int n = tree_n[r];
+  double *raw = (double *)(smem + L.raw);
+  double *FC = (double *)(smem + L.fc);
+  uint16_t *FCOL = (uint16_t *)(smem + L.fcol);
+  uint16_t *P = (uint16_t *)(smem + L.p);
+  uint16_t *T = (uint16_t *)(smem + L.t);
+  uint32_t *stk = (uint32_t *)(smem + L.stk);
+  int *scan = (int *)(smem + L.scan);
+  for (int pos = threadIdx.x; pos < n; pos += blockDim.x) {
+    const double *t = tree_pts + 3 * (rowoff + pos);
+    FC[pos] = t[0];
+    FC[C + pos] = t[1];
+    FC[2 * C + pos] = t[2];
+    FCOL[pos] = (uint16_t)tree_col[rowoff + pos];
+  }
+  __syncthreads();
+  block_build_kdtree<uint16_t>(FC, C, n, P, T, 0);
+  // the tree in position order: back to tree_pts / tree_col, and SoA in raw
+  double *TX = raw, *TY = raw + C, *TZ = raw + 2 * C;
+  for (int pos = threadIdx.x; pos < n; pos += blockDim.x) {
+    const int e = P[pos];
+    TX[pos] = FC[e];
+    TY[pos] = FC[C + e];
+    TZ[pos] = FC[2 * C + e];
+    T[pos] = FCOL[e];
+  }
+  __syncthreads();
+  for (int pos = threadIdx.x; pos < n; pos += blockDim.x) {
+    double *o = tree_pts + 3 * (rowoff + pos);
+    o[0] = TX[pos];
+    o[1] = TY[pos];
+    o[2] = TZ[pos];
+    tree_col[rowoff + pos] = T[pos];
+  }
+  // the query row's features (its curvature, src/slam.c:11-61) -> the walk
+  double *sraw = FC;
+  uint16_t *SM = P;
+  block_copy(sraw, feat_src + 3 * rowoff, 3 * C);
+  __syncthreads();
+  for (int j = threadIdx.x; j < C; j += blockDim.x) {
+    const int f = row_curv_lds(sraw, C, j) > 0.1 ? 1 : 0;
+    SM[j] = (uint16_t)f;
+    if (!f) {
+      nn_pos[rowoff + j] = -1;
+      nn_dist[rowoff + j] = INFINITY;
+    }
+  }
+  __syncthreads();
+  uint16_t *QL = FCOL;
+  const int nq = block_compact(
+      C, scan, [&](int j) { return SM[j] != 0; },
+      [&](int j, int pos) { QL[pos] = (uint16_t)j; });
+  for (int i = threadIdx.x; i < nq; i += blockDim.x) {
+    const int c = QL[i];
+    const double *q = queries + 3 * (rowoff + c);
+    int bpos;
+    double bd;
+    kd_query(TX, TY, TZ, n, q[0], q[1], q[2], stk + threadIdx.x, blockDim.x, &bpos, &bd);
+    if (bpos >= 0) {  // the lowest position holding bit-identical coordinates
+      const long long rx = __double_as_longlong(TX[bpos]), ry = __double_as_longlong(TY[bpos]),
+                      rz = __double_as_longlong(TZ[bpos]);
+      for (int p = 0; p < bpos; ++p)
+        if (__double_as_longlong(TX[p]) == rx && __double_as_longlong(TY[p]) == ry &&
+            __double_as_longlong(TZ[p]) == rz) {
+          bpos = p;
+          break;
+        }
+    }
+    nn_pos[rowoff + c] = bpos;
+    nn_dist[rowoff + c] = bd;
   }
 }
 
@@ -2417,10 +2749,10 @@ int navgpu_transform_dev(navgpu_ctx *ctx, const double *pts, size_t n,
 }
 
 // ------------------------------------------------------------ R4-R6 rows
-int navgpu_kd_build_rows_dev(navgpu_ctx *ctx, const double *feat_src,
+static int rows_build_launch(navgpu_ctx *ctx, const double *feat_src,
                              const double *coords, int R, int C,
                              double *tree_pts, int32_t *tree_col,
-                             int32_t *tree_n, int32_t *mask_out) {
+                             int32_t *tree_n, int32_t *mask_out, int build) {
   ARG_CHECK(ctx);
   RC(check_rows_shape(R, C, false));
   if (R == 0) return NAVGPU_OK;
@@ -2435,9 +2767,23 @@ int navgpu_kd_build_rows_dev(navgpu_ctx *ctx, const double *feat_src,
   TimedRegion tr(ctx, "rows_build");
   hipLaunchKernelGGL(k_rows_build, dim3(R), dim3(kRowsBuildBlock), L.total,
                      ctx->stream, feat_src, coords, R, C, tree_pts, tree_col,
-                     tree_n, mask_out);
+                     tree_n, mask_out, build);
   CHECK_LAUNCH("k_rows_build");
   return NAVGPU_OK;
+}
+
+int navgpu_kd_build_rows_dev(navgpu_ctx *ctx, const double *feat_src,
+                             const double *coords, int R, int C,
+                             double *tree_pts, int32_t *tree_col,
+                             int32_t *tree_n, int32_t *mask_out) {
+  return rows_build_launch(ctx, feat_src, coords, R, C, tree_pts, tree_col, tree_n, mask_out, 1);
+}
+
+int navgpu_kd_compact_rows_dev(navgpu_ctx *ctx, const double *feat_src,
+                               const double *coords, int R, int C,
+                               double *tree_pts, int32_t *tree_col,
+                               int32_t *tree_n, int32_t *mask_out) {
+  return rows_build_launch(ctx, feat_src, coords, R, C, tree_pts, tree_col, tree_n, mask_out, 0);
 }
 
 int navgpu_kd_rows_nodes_dev(navgpu_ctx *ctx, const double *tree_pts,
@@ -2482,17 +2828,20 @@ void navgpu_host_free(navgpu_ctx *ctx, void *hptr) {
   (void)hipHostFree(hptr);
 }
 
-int navgpu_kd_query_rows_dev(navgpu_ctx *ctx, const double *tree_pts,
+// The per-row query over built trees (tie == nullptr), or over the
+// compacted, unbuilt rows of navgpu_kd_compact_rows_dev (tie: per-row flags,
+// then k_rows_retree on the flagged rows).
+static int rows_query_launch(navgpu_ctx *ctx, const double *tree_pts,
                              const int32_t *tree_n, const double *feat_src,
                              const double *queries, int R, int C,
                              int32_t *nn_pos, double *nn_dist,
-                             int32_t *mask_out) {
+                             int32_t *mask_out, int32_t *tie) {
   ARG_CHECK(ctx);
   RC(check_rows_shape(R, C, true));
   if ((size_t)R * C == 0) return NAVGPU_OK;
   ARG_CHECK(tree_pts && tree_n && feat_src && queries && nn_pos && nn_dist);
   const char *qt = getenv("NAVGPU_ROWS_QUERY_TREE");
-  if (!(qt && *qt && *qt != '0')) {
+  if (tie || !(qt && *qt && *qt != '0')) {
     // the screen (default): >= 1024 workgroups, >= 128 columns each (two
     // ~74 KB workgroups per CU at C = 2048)
     int S = 1;
@@ -2510,7 +2859,7 @@ int navgpu_kd_query_rows_dev(navgpu_ctx *ctx, const double *tree_pts,
     TimedRegion tr(ctx, "rows_query");
     hipLaunchKernelGGL(k_rows_query_screen<kRowsQBlock>, dim3(R, S), dim3(kRowsQBlock), lds,
                        ctx->stream, tree_pts, tree_n, feat_src, queries, R, C, nn_pos, nn_dist,
-                       mask_out);
+                       mask_out, tie);
     CHECK_LAUNCH("k_rows_query_screen");
     return NAVGPU_OK;
   }
@@ -2530,6 +2879,43 @@ int navgpu_kd_query_rows_dev(navgpu_ctx *ctx, const double *tree_pts,
   hipLaunchKernelGGL(k_rows_query, dim3(R, S), dim3(kRowsQBlock), lds, ctx->stream,
                      tree_pts, tree_n, feat_src, queries, R, C, nn_pos, nn_dist, mask_out);
   CHECK_LAUNCH("k_rows_query");
+  return NAVGPU_OK;
+}
+
+int navgpu_kd_query_rows_dev(navgpu_ctx *ctx, const double *tree_pts,
+                             const int32_t *tree_n, const double *feat_src,
+                             const double *queries, int R, int C,
+                             int32_t *nn_pos, double *nn_dist,
+                             int32_t *mask_out) {
+  return rows_query_launch(ctx, tree_pts, tree_n, feat_src, queries, R, C, nn_pos, nn_dist,
+                           mask_out, nullptr);
+}
+
+int navgpu_kd_query_rows_lazy_dev(navgpu_ctx *ctx, double *tree_pts, int32_t *tree_col,
+                                  const int32_t *tree_n, const double *feat_src,
+                                  const double *queries, int R, int C, int32_t *nn_pos,
+                                  double *nn_dist, int32_t *mask_out) {
+  ARG_CHECK(ctx);
+  RC(check_rows_shape(R, C, true));
+  if ((size_t)R * C == 0) return NAVGPU_OK;
+  ARG_CHECK(tree_col);
+  int32_t *tie;
+  RC(ws(ctx, kRowTie, (size_t)R, &tie));
+  HIP_TRY(hipMemsetAsync(tie, 0, 4 * (size_t)R, ctx->stream));
+  RC(rows_query_launch(ctx, tree_pts, tree_n, feat_src, queries, R, C, nn_pos, nn_dist,
+                       mask_out, tie));
+  const RowsLds L = rows_lds(C, kRowsBlock, true);
+  if (L.total > lds_limit()) {
+    set_err("rows_query_lazy: C=%d needs %d B of LDS (device limit %d)", C, L.total,
+            lds_limit());
+    return NAVGPU_ERANGE;
+  }
+  RC(set_lds(k_rows_retree, L.total));
+  TimedRegion tr(ctx, "rows_retree");
+  hipLaunchKernelGGL(k_rows_retree, dim3(R), dim3(kRowsBlock), L.total, ctx->stream, tree_pts,
+                     tree_col, tree_n, feat_src, queries, C, nn_pos, nn_dist,
+                     (const int32_t *)tie);
+  CHECK_LAUNCH("k_rows_retree");
   return NAVGPU_OK;
 }
 
@@ -2641,13 +3027,23 @@ int rows_match_launch(navgpu_ctx *ctx, const double *src, const double *tgt, int
                          dim3(kCurvTile), 0, ctx->stream, J, nr, C);
       CHECK_LAUNCH("k_curvature");
     }
-    const int lds = rows_screen_lds(C, w);
+    const char *f32e = getenv("NAVGPU_SCREEN_F32");
+    const bool f32 = !(f32e && *f32e == '0');
+    const int lds = f32 ? rows_screen32_lds(C, w) : rows_screen_lds(C, w);
     if (lds > lds_limit()) {
       set_err("rows_screen: C=%d needs %d B of LDS (device limit %d)", C, lds, lds_limit());
       return NAVGPU_ERANGE;
     }
     const char *nte = getenv("NAVGPU_SCREEN_NT");
-    if (nte ? atoi(nte) == 512 : w >= 512) {
+    if (f32 && (nte ? atoi(nte) == 512 : w >= 512)) {
+      RC(set_lds(k_rows_screen32<512>, lds));
+      hipLaunchKernelGGL(k_rows_screen32<512>, dim3(rows, S), dim3(512), lds, ctx->stream, src,
+                         tgt, R, C, src_mask, tgt_mask, nn_idx, nn_dist, tf);
+    } else if (f32) {
+      RC(set_lds(k_rows_screen32<256>, lds));
+      hipLaunchKernelGGL(k_rows_screen32<256>, dim3(rows, S), dim3(256), lds, ctx->stream, src,
+                         tgt, R, C, src_mask, tgt_mask, nn_idx, nn_dist, tf);
+    } else if (nte ? atoi(nte) == 512 : w >= 512) {
       RC(set_lds(k_rows_screen<512>, lds));
       hipLaunchKernelGGL(k_rows_screen<512>, dim3(rows, S), dim3(512), lds, ctx->stream, src,
                          tgt, R, C, src_mask, tgt_mask, nn_idx, nn_dist, tf);

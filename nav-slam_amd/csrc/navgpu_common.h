@@ -148,6 +148,53 @@ __device__ __forceinline__ int block_excl_scan(int v, int *scratch, int *total) 
   return res;
 }
 
+// ---- packed-f32 screens with an f64 certificate (knn.hip k_knnw, the row
+// screen k_rows_screen32) ----
+typedef float f2 __attribute__((ext_vector_type(2)));
+
+// sqrt(v) rounded up by more than v_sqrt_f32's 1-ulp error: an upper bound
+// for the error terms below (they only need to bound, not be exact)
+__device__ __forceinline__ double sqrt_up(double v) {
+  return (double)__builtin_amdgcn_sqrtf((float)v) * (1.0 + 0x1p-20);
+}
+
+// Error of the packed-f32 squared distance: each coordinate is rounded to f32
+// once relative to the tile origin (<= 2^-24 |v|) and subtracted once in f32,
+// so each difference is within dl = Dq 2^-22 of the exact one (Dq bounds the
+// magnitudes); then |d2_f32 - d2| <= err(d2_f32-ish) below.
+__device__ __forceinline__ double f32_err(double V, double dl) {
+  return V * 0x1p-20 + 4.0 * dl * sqrt_up(V) + 4.0 * dl * dl;
+}
+
+// f32 admission bound for an f64 dsq bound T: every candidate whose exact
+// dsq is <= T has an f32 dsq <= the returned value.
+__device__ __forceinline__ float f32_bound(double T, double dl) {
+  if (!(T < INFINITY)) return INFINITY;
+  const double E = T * 0x1p-20 + 4.0 * dl * sqrt_up(T) + 4.0 * dl * dl;
+  return (float)((T + E) * (1.0 + 0x1p-20));
+}
+
+// the converse: an upper bound on the exact dsq of a candidate whose f32 dsq
+// is <= V (each coordinate difference within dl of the exact one)
+__device__ __forceinline__ double f32_upper(double V, double dl) {
+  return (V + f32_err(V, dl)) * (1.0 + 0x1p-20);
+}
+
+constexpr uint32_t kNoKey32 = 0xffffffffu;  // an empty key slot
+
+__device__ __forceinline__ uint32_t umed3(uint32_t a, uint32_t b, uint32_t c) {
+  return max(min(a, b), min(max(a, b), c));  // one v_med3_u32
+}
+
+// key = (f32 distance bits with the low kKeyBits cleared) | local id, as ONE
+// v_and_or_b32 (the mask in a VGPR, the id in an SGPR). lid MUST be
+// wave-uniform: a divergent value would be read from the first lane only.
+__device__ __forceinline__ uint32_t knn_key(float d, uint32_t vmask, uint32_t lid) {
+  uint32_t k;
+  asm("v_and_or_b32 %0, %1, %2, %3" : "=v"(k) : "v"(__float_as_uint(d)), "v"(vmask), "s"(lid));
+  return k;
+}
+
 }  // namespace
 
 // ------------------------------------------------------------------ host

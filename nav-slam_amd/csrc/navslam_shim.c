@@ -325,6 +325,7 @@ typedef struct {
     double h_sums[6 * ROWS];
     int32_t *d_tcol, *d_tn, *d_pos, *d_count;
     int have_trees;
+    int lazy; /* the rows hold compacted features, trees only where ties need them */
     double prof_t0; /* NAVSLAM_PROFILE */
     int32_t *d_off;         /* row offsets of the node image (ROWS+1) */
     void *d_nodes;          /* KDNode image of the row trees, device */
@@ -408,8 +409,16 @@ static void map_frame(SLAM_attr *attr, slam_state *s, Pos pos,
     CK(navgpu_upload(c, s->d_lidar, &lidar->ToF_position[0][0], 24 * NPTS));
     CK(navgpu_transform_dev(c, s->d_lidar, NPTS, R, t, NULL, s->d_global, NULL));
     CK(navgpu_side_mark(c)); /* the map slot is final here */
-    CK(navgpu_kd_build_rows_dev(c, s->d_lidar, s->d_global, ROWS, COLS,
-                                s->d_tree, s->d_tcol, s->d_tn, NULL));
+    /* without host trees nobody walks a tree the next localisation does not
+     * need: the rows keep their features in column order and only rows with
+     * a distance tie get the reference's tree (navgpu_kd_query_rows_lazy_dev) */
+    s->lazy = !host_trees();
+    if (s->lazy)
+        CK(navgpu_kd_compact_rows_dev(c, s->d_lidar, s->d_global, ROWS, COLS,
+                                      s->d_tree, s->d_tcol, s->d_tn, NULL));
+    else
+        CK(navgpu_kd_build_rows_dev(c, s->d_lidar, s->d_global, ROWS, COLS,
+                                    s->d_tree, s->d_tcol, s->d_tn, NULL));
     /* the map slot comes back while the trees build */
     CK(navgpu_side_download(c, &attr->globalPointCloud[slot].ToF_position[0][0],
                             s->d_global, 24 * NPTS));
@@ -580,8 +589,12 @@ Pos slam_localization(SLAM_attr *attr, PointCloud *lidarPointCloud,
         CK(navgpu_upload(c, s->d_tn, (int32_t[ROWS]){0}, 4 * ROWS));
         s->have_trees = 1;
     }
-    CK(navgpu_kd_query_rows_dev(c, s->d_tree, s->d_tn, s->d_lidar, s->d_last,
-                                ROWS, COLS, s->d_pos, s->d_dist, NULL));
+    if (s->lazy)
+        CK(navgpu_kd_query_rows_lazy_dev(c, s->d_tree, s->d_tcol, s->d_tn, s->d_lidar,
+                                         s->d_last, ROWS, COLS, s->d_pos, s->d_dist, NULL));
+    else
+        CK(navgpu_kd_query_rows_dev(c, s->d_tree, s->d_tn, s->d_lidar, s->d_last,
+                                    ROWS, COLS, s->d_pos, s->d_dist, NULL));
     if (adam_fast())
         return localization_fast(attr, s, transform, pos_last);
     /* GPU: the reference's correspondence list (src/slam.c:235-284), built

@@ -45,6 +45,10 @@ def _declare(L):
                                                _vp, _vp, _vp, _vp]),
         "navgpu_kd_query_rows_dev": (C.c_int, [_vp, _vp, _vp, _vp, _vp, C.c_int,
                                                C.c_int, _vp, _vp, _vp]),
+        "navgpu_kd_compact_rows_dev": (C.c_int, [_vp, _vp, _vp, C.c_int, C.c_int,
+                                                 _vp, _vp, _vp, _vp]),
+        "navgpu_kd_query_rows_lazy_dev": (C.c_int, [_vp, _vp, _vp, _vp, _vp, _vp,
+                                                    C.c_int, C.c_int, _vp, _vp, _vp]),
         "navgpu_rows_corr_dev": (C.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, C.c_int,
                                            C.c_int, _vp, _vp]),
         "navgpu_rows_corr_list_dev": (C.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, C.c_int,
@@ -269,6 +273,19 @@ class NavGpu:
         self._check(self.L.navgpu_kd_query_rows_dev(
             self.h, _ptr(tree_pts), _ptr(tree_n), _ptr(feat_src), _ptr(queries), R, Cc,
             _ptr(nn_pos), _ptr(nn_dist), _ptr(mask)), "kd_query_rows_dev")
+
+    def kd_compact_rows_dev(self, feat_src, coords, R, Cc, tree_pts, tree_col, tree_n,
+                            mask=None):
+        self._check(self.L.navgpu_kd_compact_rows_dev(
+            self.h, _ptr(feat_src), _ptr(coords), R, Cc, _ptr(tree_pts), _ptr(tree_col),
+            _ptr(tree_n), _ptr(mask)), "kd_compact_rows_dev")
+
+    def kd_query_rows_lazy_dev(self, tree_pts, tree_col, tree_n, feat_src, queries, R, Cc,
+                               nn_pos, nn_dist, mask=None):
+        self._check(self.L.navgpu_kd_query_rows_lazy_dev(
+            self.h, _ptr(tree_pts), _ptr(tree_col), _ptr(tree_n), _ptr(feat_src),
+            _ptr(queries), R, Cc, _ptr(nn_pos), _ptr(nn_dist), _ptr(mask)),
+            "kd_query_rows_lazy_dev")
 
     def rows_corr_dev(self, tree_pts, tree_n, nn_pos, nn_dist, ori, R, Cc, keep, sums):
         self._check(self.L.navgpu_rows_corr_dev(

@@ -157,6 +157,33 @@ int navgpu_kd_build_rows_dev(navgpu_ctx *ctx, const double *feat_src, const doub
     return NAVGPU_OK;
 }
 
+/* compacted rows in column order (no permutation) */
+int navgpu_kd_compact_rows_dev(navgpu_ctx *ctx, const double *feat_src, const double *coords,
+                               int R, int C, double *tree_pts, int32_t *tree_col,
+                               int32_t *tree_n, int32_t *mask_out)
+{
+    (void)ctx;
+    const size_t N = (size_t)R * C;
+    int *feat = malloc(sizeof(int) * (N ? N : 1));
+    int *cols = malloc(sizeof(int) * (C ? C : 1));
+    if (!feat || !cols)
+        return NAVGPU_ENOMEM;
+    orc_extract_feature(feat_src, R, C, feat, NULL);
+    for (int r = 0; r < R; r++) {
+        size_t n = orc_flatten_row(coords + 3 * (size_t)r * C, feat + (size_t)r * C, C,
+                                   tree_pts + 3 * (size_t)r * C, cols);
+        for (size_t i = 0; i < n; i++)
+            tree_col[(size_t)r * C + i] = cols[i];
+        tree_n[r] = (int32_t)n;
+    }
+    if (mask_out)
+        for (size_t g = 0; g < N; g++)
+            mask_out[g] = feat[g];
+    free(feat);
+    free(cols);
+    return NAVGPU_OK;
+}
+
 typedef struct {
     double x, y, z;
     uint64_t left, right;
@@ -318,4 +345,26 @@ int navgpu_rows_corr_dev(navgpu_ctx *ctx, const double *tree_pts, const int32_t 
     free(o_dist);
     free(o_grid);
     return NAVGPU_OK;
+}
+
+/* the lazy query: here every row gets its tree (the device builds only the
+ * rows with a tie; the answers' coordinates are the same either way) */
+int navgpu_kd_query_rows_lazy_dev(navgpu_ctx *ctx, double *tree_pts, int32_t *tree_col,
+                                  const int32_t *tree_n, const double *feat_src,
+                                  const double *queries, int R, int C, int32_t *nn_pos,
+                                  double *nn_dist, int32_t *mask_out)
+{
+    int *cols = malloc(sizeof(int) * (C ? C : 1));
+    if (!cols)
+        return NAVGPU_ENOMEM;
+    for (int r = 0; r < R; r++) {
+        for (int i = 0; i < tree_n[r]; i++)
+            cols[i] = tree_col[(size_t)r * C + i];
+        orc_kd_build(tree_pts + 3 * (size_t)r * C, cols, (size_t)tree_n[r]);
+        for (int i = 0; i < tree_n[r]; i++)
+            tree_col[(size_t)r * C + i] = cols[i];
+    }
+    free(cols);
+    return navgpu_kd_query_rows_dev(ctx, tree_pts, tree_n, feat_src, queries, R, C, nn_pos,
+                                    nn_dist, mask_out);
 }

@@ -2,13 +2,14 @@
 # Build experimental libnavgpu variants (compile-time knobs, phase stamps,
 # timing-only ablations) into nav-slam_amd/lib/variants/ for
 # knn_probe.py --lib / knn_sweep.py.
-# usage: scripts/build_variants.sh [name:"-DFLAG -DFLAG2" ...]  (default: stamps + k-NN ablations)
+# usage: [VDIR=dir] scripts/build_variants.sh [name:"-DFLAG -DFLAG2" ...]  (default: stamps + k-NN ablations)
 cd "$(dirname "$0")/.." || exit 1
-rm -rf nav-slam_amd/lib/variants; mkdir -p nav-slam_amd/lib/variants
+VDIR=${VDIR:-nav-slam_amd/lib/variants}
+rm -rf "$VDIR"; mkdir -p "$VDIR"
 build() {  # build <name> <defines...>
   local name=$1; shift
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -fPIC \
-    -Iinclude "$@" -shared -o "nav-slam_amd/lib/variants/libnavgpu_$name.so" \
+    -Iinclude "$@" -shared -o "$VDIR/libnavgpu_$name.so" \
     nav-slam_amd/csrc/navgpu.hip nav-slam_amd/csrc/knn.hip &
 }
 if [ $# -gt 0 ]; then
@@ -19,4 +20,4 @@ else
   build noexact -DNAVGPU_ABL=2
 fi
 wait
-ls nav-slam_amd/lib/variants
+ls "$VDIR"

@@ -2,7 +2,7 @@
 # r4: k-NN GPU tests, then the variant probe A/B, then the bench of the default
 TAG=${1:-r4s2}; OUT=gpurun_out/$TAG; mkdir -p "$OUT"
 export NAVSLAM_QUIET=1 PYTHONUNBUFFERED=1
-timeout -k 10 400 python3 -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread \
+timeout -k 10 ${PYT_LIMIT:-400} python3 -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread \
   -k "${PYTEST_K:-knn or pair or smoke}" > "$OUT/pytest.log" 2>&1; rc=$?
 echo "pytest rc=$rc"; tail -n 3 "$OUT/pytest.log"; [ $rc -ne 0 ] && exit $rc
 bash scripts/r4_var.sh "$TAG/v" ${ROUNDS:-2} || exit $?

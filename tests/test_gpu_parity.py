@@ -412,6 +412,61 @@ def test_split_build_query_vs_oracle(gpu, orc, monkeypatch, query_tree):
         assert (pos[r][qm[r] == 0] == -1).all()
 
 
+@pytest.mark.parametrize("seed,integer_mm", [(21, True), (5, False)])
+def test_lazy_rows_vs_oracle(gpu, orc, seed, integer_mm):
+    """kd_compact_rows_dev + kd_query_rows_lazy_dev (the shim's K5 path with
+    NAVSLAM_HOST_TREES=0): a row stays in column order unless one of its
+    queries met a distance tie, and then holds the reference's tree (and
+    column map) exactly; every query's distance equals the oracle's KD walk
+    and its position holds the coordinates of the reference's Point.
+    Integer-millimetre ranges make ties common (some rows must be rebuilt)."""
+    import torch
+    from navslam.synth import l9_pair
+    R, Cc = 64, 1024
+    lid, lid2 = l9_pair(R, Cc, seed=seed, integer_mm=integer_mm)
+    Rm = orc.rotation(1.5, -0.7, 12.0)
+    coords = np.einsum("ij,rcj->rci", Rm.reshape(3, 3), lid) + np.array([100.0, -20.0, 3.0])
+    dev = torch.device("cuda")
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+    d_lid, d_coords, d_lid2 = t(lid), t(coords), t(lid2)
+    tree = torch.zeros((R, Cc, 3), dtype=torch.float64, device=dev)
+    tcol = torch.zeros((R, Cc), dtype=torch.int32, device=dev)
+    tn = torch.zeros(R, dtype=torch.int32, device=dev)
+    mask = torch.zeros((R, Cc), dtype=torch.int32, device=dev)
+    gpu.kd_compact_rows_dev(d_lid, d_coords, R, Cc, tree, tcol, tn, mask)
+    pos = torch.zeros((R, Cc), dtype=torch.int32, device=dev)
+    dist = torch.zeros((R, Cc), dtype=torch.float64, device=dev)
+    qmask = torch.zeros((R, Cc), dtype=torch.int32, device=dev)
+    gpu.kd_query_rows_lazy_dev(tree, tcol, tn, d_lid2, d_lid2, R, Cc, pos, dist, qmask)
+    gpu.sync()
+    fm = orc.extract_feature(lid)
+    _eq(mask.cpu().numpy(), fm, "build mask")
+    qm = orc.extract_feature(lid2)
+    _eq(qmask.cpu().numpy(), qm, "query mask")
+    tree, tn, pos, dist = tree.cpu().numpy(), tn.cpu().numpy(), pos.cpu().numpy(), dist.cpu().numpy()
+    tcol = tcol.cpu().numpy()
+    rebuilt = 0
+    for r in range(R):
+        cols = np.nonzero(fm[r] == 1)[0]
+        n = len(cols)
+        assert tn[r] == n
+        rt, rix = orc.kd_build(coords[r, cols])
+        if (tcol[r, :n] == cols).all() and tree[r, :n].tobytes() == coords[r, cols].tobytes():
+            pass  # left in column order
+        else:
+            rebuilt += 1
+            _eq(tree[r, :n], rt, f"row {r} rebuilt tree")
+            _eq(tcol[r, :n], cols[rix], f"row {r} rebuilt cols")
+        for c in np.nonzero(qm[r] == 1)[0]:
+            p, d = orc.kd_nn(rt, lid2[r, c])
+            assert (pos[r, c] >= 0) == (p >= 0) and dist[r, c] == d, (r, c)
+            if p >= 0:
+                assert tree[r, pos[r, c]].tobytes() == rt[p].tobytes(), (r, c)
+        assert (pos[r][qm[r] == 0] == -1).all()
+    if integer_mm:
+        assert rebuilt > 0, rebuilt
+
+
 # ---------------------------------------------------------- global k-NN
 @pytest.mark.parametrize("k", [1, 3, 8, 16])
 def test_knn_vs_brute(gpu, orc, k):
@@ -712,10 +767,33 @@ def test_shim_l5_stream_matches_reference_golden(golden, monkeypatch):
             off += n
 
 
-@pytest.mark.parametrize("R,Cc,frames", [(54, 42, 12), (128, 2048, 4)])
-def test_shim_stream_vs_oracle(monkeypatch, R, Cc, frames):
-    """Larger grids (L9 54x42, K2 128x2048): shim vs the oracle frame loop."""
+def test_shim_l5_stream_lazy_rows_match_reference_golden(golden, monkeypatch):
+    """The same golden trace with NAVSLAM_HOST_TREES=0 (no KDNode trees
+    handed out; the device rows hold compacted features and a row gets its
+    tree only when a query meets a distance tie): poses, errors and the map
+    unchanged, kdtree_lastframe left NULL."""
     monkeypatch.setenv("NAVSLAM_QUIET", "1")
+    monkeypatch.setenv("NAVSLAM_HOST_TREES", "0")
+    from shimlib import Shim
+    g = golden("slam8x8")
+    out = _run_shim_stream(Shim(8, 8), g["depth"], g["imu"])
+    _eq(np.array(out["meas"]), g["pos_meas"], "pos_measure trace")
+    _eq(np.array(out["fused"]), g["pos_fused"], "fused pose trace")
+    _eq(np.array(out["err"]), g["error"], "registration error")
+    assert out["frame_count"] == int(g["frame_count"])
+    _eq(out["last_global"], g["last_global"], "globalPointCloud")
+    assert all(len(t) == 0 for fr in out["trees"] for t in fr)
+
+
+@pytest.mark.parametrize("trees", ["1", "0"])
+@pytest.mark.parametrize("R,Cc,frames", [(54, 42, 12), (128, 2048, 4)])
+def test_shim_stream_vs_oracle(monkeypatch, R, Cc, frames, trees):
+    """Larger grids (L9 54x42, K2 128x2048): shim vs the oracle frame loop,
+    with the host KDNode trees built every frame (NAVSLAM_HOST_TREES=1) and
+    with the lazy device rows (=0: compacted rows, a tree only for a row whose
+    screen met a distance tie)."""
+    monkeypatch.setenv("NAVSLAM_QUIET", "1")
+    monkeypatch.setenv("NAVSLAM_HOST_TREES", trees)
     from pyoracle import Oracle, OracleEkf, OracleSlam
     from shimlib import Shim
     orc = Oracle()
@@ -748,13 +826,16 @@ def test_shim_stream_vs_oracle(monkeypatch, R, Cc, frames):
     _eq(got["last_global"], s.last_global(), "last global frame")
 
 
+@pytest.mark.parametrize("trees", ["1", "0"])
 @pytest.mark.parametrize("R,Cc,F,steps", [(54, 42, 4, 9), (128, 2048, 3, 4)])
-def test_shim_l9_stream_vs_oracle(monkeypatch, R, Cc, F, steps):
+def test_shim_l9_stream_vs_oracle(monkeypatch, R, Cc, F, steps, trees):
     """K5 shape: the L9 loop of src/main.c:423-431 (localization with
     pred = last, then mapping at the measured pose) over a ray-cast stream
     replayed back and forth, through the drop-in ABI; every pose, error and
-    the frame stats bit-exact against the oracle's slam.c restatement."""
+    the frame stats bit-exact against the oracle's slam.c restatement, with
+    host trees on and off (lazy rows)."""
     monkeypatch.setenv("NAVSLAM_QUIET", "1")
+    monkeypatch.setenv("NAVSLAM_HOST_TREES", trees)
     from pyoracle import Oracle, OracleSlam
     from shimlib import Pos, Shim
     from navslam.synth import l9_stream, l9_stream_index
@@ -955,14 +1036,16 @@ def test_rows_corr_list_matches_reference_list(gpu, orc, integer_mm):
     _eq(got[:, 6], d, "distance")
 
 
+@pytest.mark.parametrize("trees", ["1", "0"])
 @pytest.mark.parametrize("R,Cc,F,steps", [(54, 42, 4, 9), (128, 2048, 3, 4)])
-def test_shim_l9_stream_fast_adam(monkeypatch, R, Cc, F, steps):
+def test_shim_l9_stream_fast_adam(monkeypatch, R, Cc, F, steps, trees):
     """NAVSLAM_ADAM=fast (GPU dedup + closed-form Adam sums) on the K5 loop:
     the same correspondence counts as the oracle's slam.c restatement every
     frame, poses within 1e-6 mm / deg (tolerance of the order-free sums,
     which round differently from the reference's sequential ones)."""
     monkeypatch.setenv("NAVSLAM_QUIET", "1")
     monkeypatch.setenv("NAVSLAM_ADAM", "fast")
+    monkeypatch.setenv("NAVSLAM_HOST_TREES", trees)
     from pyoracle import Oracle, OracleSlam
     from shimlib import Pos, Shim
     from navslam.synth import l9_stream, l9_stream_index
@@ -989,7 +1072,8 @@ def test_shim_l9_stream_fast_adam(monkeypatch, R, Cc, F, steps):
         last_g, last_o = meas, om
 
 
-def test_shim_l9_long_stream_crosses_map_ring(monkeypatch):
+@pytest.mark.parametrize("trees", ["1", "0"])
+def test_shim_l9_long_stream_crosses_map_ring(monkeypatch, trees):
     """K5 past the reference's 100-frame map (headers/slam.h:12; src/slam.c:395
     writes globalPointCloud[frameCount] unbounded, the shim keeps a ring):
     the L9 loop at 54x42 for 120 frames, every pose, error and frame stat
@@ -997,6 +1081,7 @@ def test_shim_l9_long_stream_crosses_map_ring(monkeypatch):
     and the ring slot of the last frame equal to the oracle's last map."""
     monkeypatch.setenv("NAVSLAM_QUIET", "1")
     monkeypatch.delenv("NAVSLAM_ADAM", raising=False)
+    monkeypatch.setenv("NAVSLAM_HOST_TREES", trees)
     from pyoracle import Oracle, OracleSlam
     from shimlib import Pos, Shim
     from navslam.synth import l9_stream, l9_stream_index
