@@ -305,7 +305,7 @@ def run_k5(a, ws, rank, dev):
     from navslam.gpu import load_library
     L = load_library()
     L.navgpu_timing_enable(ctx, 1)
-    names = ["rows_build", "rows_query"] + (["rows_corr"] if a.k5_mode == "fast" else [])
+    names = ["rows_build", "rows_query", "rows_retree"] + (["rows_corr"] if a.k5_mode == "fast" else [])
     for n in names:
         L.navgpu_timing_read(ctx, n.encode(), 1)
     q0 = state["q"]
@@ -344,7 +344,7 @@ def run_k5(a, ws, rank, dev):
     roof = {"bound": "hbm", "achieved": round(ach, 2) if ach else None, "peak": HBM_PEAK_GBS,
             "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 6) if ach else None,
             "traffic": tj and tj.get("bytes_per_step"),
-            "kernel": "k_rows_build + k_rows_query (+ k_rows_corr) per frame",
+            "kernel": "k_rows_build + k_rows_query (+ k_rows_retree, k_rows_corr) per frame",
             "avg_us": round(gpu_us, 2), "bytes_per_launch": bytes_pf,
             "bytes_model": "24 B/target feature (build) + 24 Q + 24 T + 12 Q (query), SURVEY 8d",
             "note": ("latency-bound per-row kernels; " + ("a frame is host-bound (sequential "
@@ -361,6 +361,9 @@ def run_k5(a, ws, rank, dev):
                                    + ("bit-exact host dedup + Adam" if a.k5_mode == "exact" else
                                       "GPU dedup + closed-form Adam sums (NAVSLAM_ADAM=fast)")),
                       "k5_mode": a.k5_mode,
+                      # NAVSLAM_HOST_TREES=0: no KDNode trees handed to the
+                      # caller, row trees built only for rows with a tie (r4)
+                      "host_trees": os.environ.get("NAVSLAM_HOST_TREES", "1") != "0",
                       "parallelism": f"replicas x{ws}", "points_per_frame": R * Cc,
                       "frames_per_s": round(frames_all / elapsed, 2),
                       "queries_per_frame": round(qpf, 1), "mode": "rows"},

@@ -140,7 +140,13 @@ __device__ __forceinline__ int tape_jump(int p, int sp, unsigned long long lbelo
                                          int wave_p0) {
   const int k = p - sp;  // >= 1
   const int s = lbelow ? wave_p0 + kWave - __clzll(lbelow) : wave_p0;
-  return p - k * ((p - s + k) / k);
+  // (p - s + k) / k exactly: the f32 reciprocal's quotient is within one of
+  // it for operands below 2^24, then one correction (no integer divide)
+  const int a = p - s + k;
+  int q = (int)((float)a * __builtin_amdgcn_rcpf((float)k));
+  const int r = a - q * k;
+  q += r >= k ? 1 : (r < 0 ? -1 : 0);
+  return p - k * q;
 }
 
 template <class IdxT, bool GMEM = false>
@@ -225,8 +231,13 @@ constexpr int kBlockNthMax = 1024;
 // windows this short finish on wave 0 alone (a block pass costs ~4 barriers
 // whatever its length; a wave pass over a few 64-position chunks needs none)
 constexpr int kBlockToWave = NAVGPU_BLOCK_TO_WAVE;
+// block pass form: 1 = r3 (a barrier per chunk for the counts, then
+// barrier rounds for chains that cross waves), 2 = r4 (one barrier per chunk)
+#ifndef NAVGPU_BLOCK_NTH_V
+#define NAVGPU_BLOCK_NTH_V 2
+#endif
 template <class IdxT, bool GMEM = false>
-__device__ void block_nth_element(const double *key, IdxT *P, IdxT *T, int first,
+__device__ void block_nth_element_r3(const double *key, IdxT *P, IdxT *T, int first,
                                   int last, int nth) {
   __shared__ unsigned bw[2 * kBlockNthMax];
   __shared__ int bcnt[2][kBlockNthMax / kWave];
@@ -315,6 +326,115 @@ __device__ void block_nth_element(const double *key, IdxT *P, IdxT *T, int first
     else
       last = i - 1;
   }
+}
+
+template <class IdxT, bool GMEM = false>
+__device__ void block_nth_element(const double *key, IdxT *P, IdxT *T, int first,
+                                  int last, int nth) {
+#if NAVGPU_BLOCK_NTH_V == 1
+  block_nth_element_r3<IdxT, GMEM>(key, P, T, first, last, nth);
+#else
+  // r4: ONE barrier per chunk. Before it every wave publishes its small and
+  // large ballots, its small count and the chunk's elements (E); after it a
+  // lane follows its tape chain by itself: a run of smalls is one tape_jump,
+  // a position of an earlier chunk reads its final T, a large position or a
+  // fixed point (sp == p) reads E, and a small position of another wave of
+  // this chunk takes that wave's ballots from LDS and jumps again (on scan
+  // rows 59 % of the waves need no hop and the mean of a wave's longest
+  // chain is 1.5 hops). The buffers alternate between chunks, so a wave one
+  // chunk ahead never overwrites what a slower wave still reads.
+  constexpr int NWM = kBlockNthMax / kWave;
+  __shared__ unsigned long long bsb[2][NWM], blb[2][NWM];
+  __shared__ int bcn[2][NWM];
+  __shared__ uint32_t bel[2][kBlockNthMax];
+  __shared__ int bpre[NWM][NWM + 1];  // per wave: its copy of the chunk's wave prefix
+  const int tid = threadIdx.x, lane = tid & (kWave - 1), wid = tid / kWave;
+  const int bd = blockDim.x, nw = bd / kWave, wbase = wid * kWave;
+  const unsigned long long below = (1ull << lane) - 1ull;
+  int chunk = 0;
+  while (first < last) {
+    if (last - first < kBlockToWave) {
+      if (wid == 0) wave_nth_element<IdxT, GMEM>(key, P, T, first, last, nth, lane);
+      if (GMEM) __threadfence_block();
+      __syncthreads();
+      return;
+    }
+    const int pe = (int)P[last];
+    const double pk = key[pe];
+    const int m = last - first;
+    int S = 0;
+    int e_n = tid < m ? (int)P[first + tid] : 0;
+    double k_n = key[e_n];
+    for (int cs = 0; cs < m; cs += bd, ++chunk) {
+      const int b = chunk & 1;
+      const int p = cs + tid;
+      const bool act = p < m;
+      const int e = e_n;
+      const bool small = act && ((k_n - pk) <= 0.0);  // kdtree.c:31-43
+      if (cs + bd < m) {  // the next chunk's reads (this chunk writes below it)
+        const int pn = p + bd;
+        e_n = pn < m ? (int)P[first + pn] : 0;
+        k_n = key[e_n];
+      }
+      const unsigned long long bal = __ballot(small);
+      const unsigned long long lbal = __ballot(act && !small);
+      bel[b][tid] = (uint32_t)e;
+      if (lane == 0) {
+        bsb[b][wid] = bal;
+        blb[b][wid] = lbal;
+        bcn[b][wid] = __popcll(bal);
+      }
+      __syncthreads();
+      // the chunk's wave prefix (lane x of every wave: smalls in waves < x)
+      int c = lane < nw ? bcn[b][lane] : 0;
+      int incl = c;
+#pragma unroll
+      for (int o = 1; o < NWM; o <<= 1) {
+        const int t = __shfl_up(incl, o, kWave);
+        if (lane >= o) incl += t;
+      }
+      if (lane <= nw) bpre[wid][lane] = incl - c;  // lane nw: the chunk's total
+      wave_sync_mem();
+      const int before = bpre[wid][wid], tot = bpre[wid][nw];
+      const int sp = S + before + lanes_below(bal);
+      uint32_t w = (uint32_t)e;
+      if (small && sp != p) {
+        int y = tape_jump(p, sp, lbal & below, cs + wbase);
+        for (;;) {
+          if (y < cs) {
+            w = (uint32_t)T[first + y];
+            break;
+          }
+          const int wy = (y - cs) >> 6, ly = (y - cs) & (kWave - 1);
+          const unsigned long long yb = (1ull << ly) - 1ull;
+          const unsigned long long ysb = bsb[b][wy], ylb = blb[b][wy];
+          const int spy = S + bpre[wid][wy] + __popcll(ysb & yb);
+          if (((ylb >> ly) & 1ull) || spy == y) {
+            w = bel[b][y - cs];
+            break;
+          }
+          y = tape_jump(y, spy, ylb & yb, cs + (wy << 6));
+        }
+      }
+      if (act) T[first + p] = (IdxT)w;
+      if (small) P[first + sp] = (IdxT)e;
+      S += tot;
+    }
+    __syncthreads();  // the last chunk's T and P before the tape copy
+    for (int q = S + tid; q < m; q += bd) {
+      const int v = (int)T[first + q];
+      P[q == S ? last : first + q] = (IdxT)v;
+    }
+    if (tid == 0) P[first + S] = (IdxT)pe;
+    __syncthreads();
+    const int i = first + S;
+    if (i == nth) break;
+    if (i < nth)
+      first = i + 1;
+    else
+      last = i - 1;
+  }
+#endif
 }
 
 // The reference nth_element (utils/kdtree.c:20-52) run serially by one lane:

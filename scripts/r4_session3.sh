@@ -22,3 +22,6 @@ b k2_f32 "NAVGPU_SCREEN_F32=1" "--workload k2" || exit 1
 b k2_f64 "NAVGPU_SCREEN_F32=0" "--workload k2" || exit 1
 b k5f_lazy "NAVSLAM_HOST_TREES=0" "--workload k5 --k5-mode fast" || exit 1
 b k5f_trees "NAVSLAM_HOST_TREES=1" "--workload k5 --k5-mode fast" || exit 1
+b k2i "" "--workload k2 --integer-mm" || exit 1
+b k2i_nth1 "NAVGPU_LIB=nav-slam_amd/lib/var_nth/libnavgpu_nth1.so" "--workload k2 --integer-mm" || exit 1
+b k4i "" "--workload k4 --integer-mm" || exit 1

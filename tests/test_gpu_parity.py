@@ -328,12 +328,17 @@ def test_rows_match_nonfinite_and_dense_features(gpu, orc):
             _eq(a, b, f"{name}: {what}")
 
 
-def test_rows_screen_vs_tree_path(gpu, orc, monkeypatch):
+@pytest.mark.parametrize("f32", ["1", "0"])
+def test_rows_screen_vs_tree_path(gpu, orc, monkeypatch, f32):
     """The screened per-row path (exact argmin, the reference tree only for
     rows with a tie) == the tree on every row (NAVGPU_ROWS_SCREEN=0) == the
     oracle, on data that stresses the screen's argument: integer ties,
     non-finite coordinates, distances whose squares underflow, duplicate
-    points, large offsets (utils/kdtree.c:110-152)."""
+    points, large offsets (utils/kdtree.c:110-152); with the f32 pre-screen
+    (k_rows_screen32, NAVGPU_SCREEN_F32=1: its certificate must fall back to
+    the f64 scan on near-ties a few ulps apart, coordinates beyond the f32
+    range and rows whose first feature is far from the rest) and without."""
+    monkeypatch.setenv("NAVGPU_SCREEN_F32", f32)
     from navslam.synth import l9_pair
     rng = np.random.default_rng(77)
     cases = []
@@ -352,6 +357,18 @@ def test_rows_screen_vs_tree_path(gpu, orc, monkeypatch):
     cases.append(("duplicates", dup, dup[::-1].copy()))
     off = rng.uniform(0, 100, (8, 700, 3)) + 1e9
     cases.append(("offset", off, off + rng.uniform(-1, 1, off.shape)))
+    huge = rng.uniform(-1, 1, (4, 300, 3)) * np.array([1e20, 1e39, 1e300, 1e20])[:, None, None]
+    cases.append(("huge", huge, huge[:, ::-1].copy() * 0.999))
+    # near-ties: every target has a partner mirrored about the query grid
+    # plane, nudged by a few ulps (the f32 keys cannot tell them apart)
+    base = rng.uniform(-20, 20, (8, 256, 3))
+    mir = base.copy()
+    mir[..., 0] = -mir[..., 0]
+    mir = np.nextafter(mir, np.inf)
+    near_t = np.concatenate([base, mir], axis=1)
+    near_s = np.zeros_like(near_t)
+    near_s[..., 1:] = near_t[..., 1:] + rng.uniform(-0.5, 0.5, near_t[..., 1:].shape)
+    cases.append(("near-ties", near_s, near_t))
     names = ("src_mask", "tgt_mask", "nn_idx", "nn_dist")
     for label, s, t in cases:
         monkeypatch.delenv("NAVGPU_ROWS_SCREEN", raising=False)
