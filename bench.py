@@ -692,8 +692,9 @@ def main():
                     build_traffic = tj.get("build_bytes_per_step")
             roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
                     "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic,
-                    "kernel": ("query stage k_knn<%d> + k_knn_slow<%d>, one launch each per "
-                               "step" % (a.k, a.k)),
+                    "kernel": ("query stage %s<%d> + k_knn_slow<%d>, one launch each per "
+                               "step" % ("k_knn" if os.environ.get("NAVGPU_KNN_MODE") == "0"
+                                         else "k_knnw", a.k, a.k)),
                     "avg_us": round(dom_avg_us, 2), "launches": dom_n,
                     "timing": ("HIP events on each context's stream over the timed region"
                                + (f" ({nf} pairs in flight: shares the chip with the other "
@@ -709,7 +710,7 @@ def main():
             # and its measured traffic
             b_ms, b_n = kt.get("knn_build", (0.0, 0))
             if b_n:
-                bld = {"kernels": ("k_bbox_partial + k_grid_params + k_bin_hist + k_bin_colscan + "
+                bld = {"kernels": ("k_bbox_partial + k_bin_hist (with the grid) + k_bin_colscan + "
                                    "k_bin_scatter + k_bin_fine (both clouds binned)"),
                        "avg_us": round(1000.0 * b_ms / b_n, 2),
                        "bytes_model": "24 B/target read (SURVEY 8d); the query binning is extra",
@@ -793,14 +794,17 @@ def main():
     return out
 
 
-QUERY_KERNELS = ("k_knn<", "k_knn_slow<")
+QUERY_KERNELS = ("k_knnw<", "k_knn<", "k_knn_slow<")
+# the query pass launched once per step: k_knnw (r4 default) or k_knn
+# (NAVGPU_KNN_MODE=0)
+QUERY_MAIN = ("k_knnw<", "k_knn<")
 BUILD_KERNELS = ("k_bbox_partial", "k_grid_params", "k_bin_hist", "k_bin_colscan",
                  "k_bin_scatter", "k_bin_fine")
 # per-row workloads: the kernels of one step and the kernel launched once per
 # step (the per-step divisor)
 ROWS_KERNELS = ("k_curvature", "k_rows_screen", "k_rows_match")
-K5_KERNELS = ("k_rows_build", "k_rows_query", "k_rows_corr")
-TRAFFIC_SETS = {"k3": (QUERY_KERNELS, "k_knn<"), "k3_build": (BUILD_KERNELS, "k_knn<"),
+K5_KERNELS = ("k_rows_build", "k_rows_query", "k_rows_retree", "k_rows_corr")
+TRAFFIC_SETS = {"k3": (QUERY_KERNELS, QUERY_MAIN), "k3_build": (BUILD_KERNELS, QUERY_MAIN),
                 "rows": (ROWS_KERNELS, "k_rows_screen"), "k5": (K5_KERNELS, "k_rows_build")}
 
 
@@ -827,7 +831,7 @@ def load_traffic(a, match):
     return tj if all(tj.get(k) == v for k, v in match.items()) else None
 
 
-def pmc_bytes(paths, kernel_subs, anchor="k_knn<"):
+def pmc_bytes(paths, kernel_subs, anchor=QUERY_MAIN):
     """HBM bytes per step of the kernels whose name contains one of
     `kernel_subs`, from rocprofv3 --pmc counter CSVs (FETCH_SIZE in one pass,
     WRITE_SIZE in another; both in KB). Per step = total / launches of the
@@ -842,7 +846,7 @@ def pmc_bytes(paths, kernel_subs, anchor="k_knn<"):
             for r in csv.DictReader(f):
                 name = r.get("Kernel_Name", "")
                 c = r.get("Counter_Name")
-                if anchor in name:
+                if any(x in name for x in ((anchor,) if isinstance(anchor, str) else anchor)):
                     launches.setdefault(c, set()).add(r.get("Dispatch_Id"))
                 if not any(k in name for k in kernel_subs):
                     continue

@@ -1,5 +1,5 @@
 """Cross-check of a K3 bench line against the rocprofv3 kernel trace of the
-same run: per launch of k_knn<K>, the summed durations of the index build
+same run: per launch of the query pass (k_knnw<K>, or k_knn<K>), the summed durations of the index build
 kernels, of the query-stage kernels and of the curvature, beside the line's
 HIP-event kernel_us (their span on the context's stream).
 
@@ -10,12 +10,12 @@ import os
 import sys
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-from bench import BUILD_KERNELS, QUERY_KERNELS  # noqa: E402
+from bench import BUILD_KERNELS, QUERY_KERNELS, QUERY_MAIN  # noqa: E402
 
 stats, line, out = sys.argv[1:4]
 rows = list(csv.DictReader(open(stats)))
 b = json.load(open(line))
-launches = sum(int(r["Calls"]) for r in rows if "k_knn<" in r["Name"])
+launches = sum(int(r["Calls"]) for r in rows if any(m in r["Name"] for m in QUERY_MAIN))
 
 
 def per_launch(keys):

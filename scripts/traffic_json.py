@@ -12,7 +12,7 @@ import os
 import sys
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-from bench import TRAFFIC_SETS, pmc_bytes  # noqa: E402
+from bench import QUERY_MAIN, TRAFFIC_SETS, pmc_bytes  # noqa: E402
 
 ap = argparse.ArgumentParser()
 ap.add_argument("fetch_csv")
@@ -31,13 +31,13 @@ note = ("bytes = FETCH_SIZE x2 (gfx950 correction, MI355X_MICROARCH.md HBM secti
 if a.workload == "k3":
     q = pmc_bytes(paths, *TRAFFIC_SETS["k3"])
     b = pmc_bytes(paths, *TRAFFIC_SETS["k3_build"])
-    main = pmc_bytes(paths, ("k_knn<",), "k_knn<")
+    main = pmc_bytes(paths, QUERY_MAIN, QUERY_MAIN)
     rec = {"workload": "k3", "k": a.k, "points_per_cloud": a.points,
            "bytes_per_step": q and q["bytes"], "build_bytes_per_step": b and b["bytes"],
            "query": q, "build": b, "k_knn_main": main,
            "kernels": {"query": list(TRAFFIC_SETS["k3"][0]),
                        "build": list(TRAFFIC_SETS["k3_build"][0])},
-           "per": "launch of k_knn<K> (one per step)"}
+           "per": "launch of the query pass k_knnw<K> / k_knn<K> (one per step)"}
 else:
     key = "k5" if a.workload.startswith("k5") else "rows"
     kern, anchor = TRAFFIC_SETS[key]

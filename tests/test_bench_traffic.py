@@ -26,8 +26,8 @@ def _pmc_csv(path, counter, rows):
                         "Counter_Value": v})
 
 
-def _k3_passes(tmp_path):
-    knn = "void (anonymous namespace)::k_knn<8>((anonymous namespace)::GridParams const*)"
+def _k3_passes(tmp_path, main="k_knn"):
+    knn = f"void (anonymous namespace)::{main}<8>((anonymous namespace)::GridParams const*)"
     slow = "void (anonymous namespace)::k_knn_slow<8>(int)"
     hist = "(anonymous namespace)::k_bin_hist((anonymous namespace)::BinJob)"
     f, w = str(tmp_path / "fetch.csv"), str(tmp_path / "write.csv")
@@ -39,8 +39,13 @@ def _k3_passes(tmp_path):
     return f, w
 
 
-def test_pmc_bytes_per_step(tmp_path):
-    f, w = _k3_passes(tmp_path)
+import pytest  # noqa: E402
+
+
+@pytest.mark.parametrize("main", ["k_knnw", "k_knn"])
+def test_pmc_bytes_per_step(tmp_path, main):
+    """k_knnw (r4 default) or k_knn (NAVGPU_KNN_MODE=0) is the per-step anchor."""
+    f, w = _k3_passes(tmp_path, main)
     q = bench.pmc_bytes([f, w], bench.QUERY_KERNELS)
     # fetch (100+4+102+2)/2 = 104 KB, write (50+1+52+1)/2 = 52 KB
     assert q == {"fetch_raw": 104 * 1024, "write": 52 * 1024, "bytes": (2 * 104 + 52) * 1024}
