@@ -25,3 +25,5 @@ b k5f_trees "NAVSLAM_HOST_TREES=1" "--workload k5 --k5-mode fast" || exit 1
 b k2i "" "--workload k2 --integer-mm" || exit 1
 b k2i_nth1 "NAVGPU_LIB=nav-slam_amd/lib/var_nth/libnavgpu_nth1.so" "--workload k2 --integer-mm" || exit 1
 b k4i "" "--workload k4 --integer-mm" || exit 1
+b k2i_t128 "NAVGPU_LIB=nav-slam_amd/lib/var_nth/libnavgpu_t128.so" "--workload k2 --integer-mm" || exit 1
+b k2i_l256 "NAVGPU_LIB=nav-slam_amd/lib/var_nth/libnavgpu_l256.so" "--workload k2 --integer-mm" || exit 1
