@@ -332,7 +332,9 @@ def run_k5(a, ws, rank, dev):
     cpu = None
     if not a.no_cpu_baseline and a.cpu_frames > 0:
         cpu = cpu_baseline_k5(frames, F, min(a.cpu_frames, len(poses)), poses)
-    per_frame = lambda n: 1000.0 * kt[n][0] / max(kt[n][1], 1)
+    # (a region never entered this run, e.g. rows_retree with host trees on,
+    # reads as count 0)
+    per_frame = lambda n: 1000.0 * kt[n][0] / kt[n][1] if kt[n][1] > 0 else 0.0
     gpu_us = sum(per_frame(n) for n in names)
     # SURVEY 8(d) bytes per frame, per-row mode: build reads 24 B per target
     # feature point + the query stage 24 B per query + 24 B per target

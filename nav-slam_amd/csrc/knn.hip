@@ -392,9 +392,19 @@ struct BinJob {
 };
 constexpr int kBinMaxShift = 15;
 constexpr int kBinUnroll = 8;  // points per thread with loads in flight
-constexpr int kBinP = 4096;    // minimum points per k_bin_hist / k_bin_scatter block
-constexpr int kBinMinShift = 10;  // coarse buckets of 2^10 cells (r2 A/B)
-constexpr int kBinFineThreads = 512;
+// (compile-time knobs for A/B variant builds, scripts/build_variants.sh)
+#ifndef NAVGPU_BIN_P
+#define NAVGPU_BIN_P 4096
+#endif
+#ifndef NAVGPU_BIN_MIN_SHIFT
+#define NAVGPU_BIN_MIN_SHIFT 10
+#endif
+#ifndef NAVGPU_BIN_FINE_THREADS
+#define NAVGPU_BIN_FINE_THREADS 512
+#endif
+constexpr int kBinP = NAVGPU_BIN_P;  // minimum points per k_bin_hist / k_bin_scatter block
+constexpr int kBinMinShift = NAVGPU_BIN_MIN_SHIFT;  // coarse buckets of 2^10 cells (r2 A/B)
+constexpr int kBinFineThreads = NAVGPU_BIN_FINE_THREADS;
 constexpr int kBinFineHold = 4096 / kBinFineThreads;  // points per thread held in registers
 
 __device__ __forceinline__ int bin_side(const BinJob &J, int &blk) {
@@ -1201,13 +1211,6 @@ constexpr int kWPairs = kWRec / 2 + 2;   // two spare pairs: read-ahead
 constexpr int kWZg = 4 * kWPairs;        // floats from the XY plane to the ZG plane
 constexpr int kWCols = 2 * kWave;        // staged columns per round: two per lane
 constexpr int kWSegs = 8;                // segments (grid rows) per round
-// waves per workgroup, each with its own chunk and LDS region (no barrier
-// between them): 1-wave workgroups measured fewer resident waves per CU than
-// their LDS allows
-#ifndef NAVGPU_KNNW_WPB
-#define NAVGPU_KNNW_WPB 2
-#endif
-constexpr int kWPB = NAVGPU_KNNW_WPB;
 #ifndef NAVGPU_KNNW_U
 #define NAVGPU_KNNW_U 1
 #endif
@@ -1248,7 +1251,7 @@ __device__ __forceinline__ WFrame wframe(const GridParams &G, int xf, int xl, in
 constexpr int kWStampChunks = 1 << 15;
 __device__ unsigned long long g_wstamps[kWStampChunks][8];
 #define NV_WFLUSH(chunk)                                             \
-  if ((threadIdx.x & 63) == 0 && (chunk) < kWStampChunks) {          \
+  if (threadIdx.x == 0 && (chunk) < kWStampChunks) {                 \
     _Pragma("unroll") for (int s_ = 1; s_ < 9; ++s_)                 \
       g_wstamps[chunk][s_ - 1] = nv_acc[s_];                         \
   }
@@ -1257,612 +1260,501 @@ __device__ unsigned long long g_wstamps[kWStampChunks][8];
 #endif
 
 template <int K>
-__global__ __launch_bounds__(kWave * kWPB, NAVGPU_KNNW_MINW) void k_knnw(
-    const GridParams *__restrict__ gp, const int *__restrict__ tstart,
-    const PRec *__restrict__ tsort, const SRec *__restrict__ srec, const QSide QS, int nq,
-    int ntg, int32_t *__restrict__ oidx, double *__restrict__ odist, KnnLists L_,
-    int *__restrict__ tickets) {
-  __shared__ __attribute__((aligned(16))) float spair_w[kWPB][2 * kWZg];
-  __shared__ int colst_w[kWPB][kWCols + 1];  // first slot of virtual column v; [kWCols] = total
+__global__ __launch_bounds__(kWave, NAVGPU_KNNW_MINW) void k_knnw(const GridParams *__restrict__ gp,
+                                                   const int *__restrict__ tstart,
+                                                   const PRec *__restrict__ tsort,
+                                                   const SRec *__restrict__ srec,
+                                                   const QSide QS, int nq, int ntg,
+                                                   int32_t *__restrict__ oidx,
+                                                   double *__restrict__ odist, KnnLists L_) {
+  __shared__ __attribute__((aligned(16))) float spair[2 * kWZg];
+  __shared__ int colst[kWCols + 1];  // first slot of virtual column v; [kWCols] = total
   // each segment's 9 row pieces: [sbnd[s][r][0], sbnd[s][r][1])
-  __shared__ int sbnd_w[kWPB][kWSegs][9][2];
-  const int wid = __builtin_amdgcn_readfirstlane((int)threadIdx.x / kWave);
-  float *const spair = spair_w[wid];
-  int *const colst = colst_w[wid];
-  int(&sbnd)[kWSegs][9][2] = sbnd_w[wid];
+  __shared__ int sbnd[kWSegs][9][2];
   constexpr int KL = K + 1;
   static_assert(K >= 1 && K <= 16, "K");
   const GridParams G = *gp;
   const int S = G.sx;
   const int g0 = G.g[0], g1 = G.g[1], g2 = G.g[2];
-  const int lane = (int)threadIdx.x & (kWave - 1);
-  const uint32_t vmask = ~kKeyMask;
-  NV_ACC_DECL;
-  NV_STAMP(w0);
-  // ---- chunk tickets: the chunks are dealt to the 8 XCDs in contiguous
-  // pools (block b runs on XCD b % 8; another placement only costs L2 hits);
-  // a wave takes the next chunk of its XCD's pool, then steals from the
-  // others. The ticket of the next chunk is drawn while this one is staged.
+  // chunks dealt to the 8 XCDs in contiguous ranges (block b -> XCD b % 8)
   const int nchunk = (nq + kWave - 1) / kWave;
   const int per = (nchunk + 7) / 8;
-  const int x0 = (int)(blockIdx.x & 7);
-  int pool = 0;
-  auto draw = [&]() -> int {  // the raw ticket of the current pool (lane 0's)
-    int t = 0;
-    if (lane == 0) t = atomicAdd(&tickets[(x0 + pool) & 7], 1);
-    return t;
-  };
-  auto resolve = [&](int t) -> int {  // a drawn ticket -> chunk, or -1 when all are done
-    t = __shfl(t, 0, kWave);
-    for (;;) {
-      const int x = (x0 + pool) & 7, lo = x * per;
-      if (t < min(per, nchunk - lo)) return lo + t;
-      if (++pool == 8) return -1;
-      t = __shfl(draw(), 0, kWave);
-    }
-  };
-  // ---- the per-chunk plan (a function of the query cells and the round's
-  // first lane): segments, virtual columns and the round's lane range
-  struct Cells {
-    int nlive, qrow, qx, qy, qz;
-    unsigned long long rowfirst, rowlast;
-  };
-  auto cells_of = [&](int chunk, int qcell) {
-    Cells C;
-    C.nlive = min(kWave, nq - chunk * kWave);
-    const bool live = lane < C.nlive;
-    // the query's cell: x, row = (z g1 + y); rows ascend over the lanes
-    C.qrow = live ? qcell / g0 : 0x7fffffff;
-    C.qx = live ? qcell - C.qrow * g0 : 0;
-    C.qy = live ? C.qrow % g1 : 0;
-    C.qz = live ? C.qrow / g1 : 0;
-    // a lane starts (ends) a grid row when the lane before (after) it holds
-    // another one (the shuffles run on every lane: a lane masked off by a
-    // short-circuit would hand its neighbour garbage)
-    const int prow = __shfl_up(C.qrow, 1, kWave), nrow = __shfl_down(C.qrow, 1, kWave);
-    C.rowfirst = __ballot(live && (lane == 0 || prow != C.qrow));
-    C.rowlast = __ballot(live && (lane == C.nlive - 1 || nrow != C.qrow));
-    return C;
-  };
-  struct Plan {
-    bool in, first;
-    int sf, sl, xf, pre, vcq, cum;  // per lane
-    int lb, NC;                     // wave-uniform
-    unsigned long long fb;
-  };
-  auto plan_of = [&](const Cells &C, int la) {
-    Plan P;
-    // segments of lanes [la, nlive): a grid row each (the first one may start
-    // mid-row after a cut round)
-    P.in = lane >= la && lane < C.nlive;
-    const unsigned long long fall = (C.rowfirst & (~0ull << la)) | (1ull << la);
+  const int chunk = (int)(blockIdx.x & 7) * per + (int)(blockIdx.x >> 3);
+  if (chunk >= nchunk) return;
+  const int lane = (int)threadIdx.x;
+  NV_ACC_DECL;
+  NV_STAMP(w0);
+  const int nlive = min(kWave, nq - chunk * kWave);
+  const int qi = chunk * kWave + lane;
+  const bool live = lane < nlive;
+  BinPt Q;
+#ifdef NAVGPU_KNNW_CHECK
+  if (live && (QS.idx[qi] < 0 || QS.idx[qi] >= nq || QS.cell[qi] < 0)) {
+    printf("knnw chunk %d lane %d: query %d idx %d cell %d\n", chunk, lane, qi, QS.idx[qi],
+           QS.cell[qi]);
+    return;
+  }
+#endif
+  Q = qload(QS, min(qi, nq - 1));  // (unconditional: see the table loads)
+  // the query's cell: x, row = (z g1 + y); rows ascend over the lanes
+  const int qrow = live ? Q.cell / g0 : 0x7fffffff;
+  const int qx = live ? Q.cell - qrow * g0 : 0;
+  const int qy = live ? qrow % g1 : 0, qz = live ? qrow / g1 : 0;
+  const uint32_t vmask = ~kKeyMask;
+  // rows ascend over the live lanes: a lane starts (ends) a grid row when the
+  // lane before (after) it holds another one (the shuffles run on every lane:
+  // a lane masked off by a short-circuit would hand its neighbour garbage)
+  const int prow = __shfl_up(qrow, 1, kWave), nrow = __shfl_down(qrow, 1, kWave);
+  const unsigned long long rowfirst = __ballot(live && (lane == 0 || prow != qrow));
+  const unsigned long long rowlast = __ballot(live && (lane == nlive - 1 || nrow != qrow));
+  NV_STAMP(w1);
+  NV_ACC(1, w0, w1);
+  for (int la = 0; la < nlive;) {
+    NV_STAMP(r0);
+    NV_ACC(7, 0ull, 1ull);
+    // ---- segments of lanes [la, nlive): a grid row each (the first one may
+    // start mid-row after a cut round)
+    const bool in = lane >= la && live;
+    const unsigned long long fall = (rowfirst & (~0ull << la)) | (1ull << la);
     const unsigned long long below = (2ull << lane) - 1;  // lanes <= lane (lane 63: all)
-    P.sf = 63 - __builtin_clzll((fall & below) | 1ull);    // the lane's segment: first lane
-    P.sl = (int)__builtin_ctzll((C.rowlast & ~(below >> 1)) | (1ull << 63));  // ... last
-    P.first = P.in && P.sf == lane;
-    const bool last = P.in && P.sl == lane;
-    P.xf = __shfl(C.qx, P.sf, kWave);  // the segment's first query cell
-    const int colq = C.qx - P.xf + S;  // the lane's cell: column in its segment
+    const int sf = 63 - __builtin_clzll((fall & below) | 1ull);  // the lane's segment: first lane
+    const int sl = (int)__builtin_ctzll((rowlast & ~(below >> 1)) | (1ull << 63));  // ... last
+    const bool first = in && sf == lane, last = in && sl == lane;
+    const int xf = __shfl(qx, sf, kWave);  // the segment's first query cell
+    const int colq = qx - xf + S;          // the lane's cell: column in its segment
     const int val = last ? colq + S + 1 : 0;  // columns of a segment, at its last lane
     const int incv = wave_scan_add(val);
-    P.pre = P.in ? incv - val : 0;  // columns of earlier segments
-    P.vcq = P.pre + colq;           // the lane's cell: virtual column
-    P.cum = P.vcq + S + 1;          // columns if the round ended here
+    const int pre = in ? incv - val : 0;   // columns of earlier segments
+    const int vcq = pre + colq;            // the lane's cell: virtual column
+    const int cum = vcq + S + 1;           // columns if the round ended here
     // the round: the lane prefix whose columns fit (cum ascends over the
     // lanes) in at most kWSegs segments
     const int segi = __popcll(fall & below) - 1;
-    P.lb = la + __popcll(__ballot(P.in && P.cum <= kWCols && segi < kWSegs));
-    P.NC = rdlane(P.cum, P.lb - 1);
-    P.fb = __ballot(P.first && lane < P.lb);  // segment starts
-    return P;
-  };
-  // virtual column v = lane + 64 p -> its cell (vx, vy, vz) and its segment's
-  // frame origin fox (x); lbc: the column-fit round's end (the frames')
-  struct Cols {
-    int vx[2], vy[2], vz[2];
-    double fox[2];
-  };
-  auto cols_of = [&](const Cells &C, const Plan &P) {
-    Cols V;
+    int lb = la + __popcll(__ballot(in && cum <= kWCols && segi < kWSegs));
+    const int lbc = lb;  // the frames use the column-fit round (a budget cut keeps them)
+    int NC = rdlane(cum, lb - 1);
+    unsigned long long fb = __ballot(first && lane < lb);  // segment starts
+    // ---- column tables: virtual column v = lane + 64 p -> cell (vx, vy, vz);
+    // cs = its records (the 9 rows'), cbr[p][r] + g = the slot of the record
+    // at cell-sorted position g of row r; dxc = the column's cell centre in
+    // its segment's frame (x)
+    int cbr[2][9], st[2][9], en[2][9];
+    float dxc[2];
+    int total;
+    {
+      int cs[2], vx[2], vy[2], vz[2];
+      double fox[2];
 #pragma unroll
-    for (int p = 0; p < 2; ++p) {
-      V.vx[p] = V.vy[p] = V.vz[p] = 0;
-      V.fox[p] = 0.0;
-    }
-    for (unsigned long long b = P.fb; b; b &= b - 1) {
-      const int f = (int)__builtin_ctzll(b);
-      const int f_vc0 = rdlane(P.pre, f), f_xf = rdlane(C.qx, f), f_x0 = f_xf - S;
-      const int f_y = rdlane(C.qy, f), f_z = rdlane(C.qz, f);
-      const int f_xl = rdlane(C.qx, min(rdlane(P.sl, f), P.lb - 1));
-      const double f_ox = wframe(G, f_xf, f_xl, f_y, f_z).o[0];
+      for (int p = 0; p < 2; ++p) {
+        vx[p] = vy[p] = vz[p] = 0;
+        cs[p] = 0;
+        fox[p] = 0.0;
+      }
+      for (unsigned long long b = fb; b; b &= b - 1) {
+        const int f = (int)__builtin_ctzll(b);
+        const int f_vc0 = rdlane(pre, f), f_xf = rdlane(qx, f), f_x0 = f_xf - S;
+        const int f_y = rdlane(qy, f), f_z = rdlane(qz, f);
+        const int f_xl = rdlane(qx, min(rdlane(sl, f), lbc - 1));
+        const double f_ox = wframe(G, f_xf, f_xl, f_y, f_z).o[0];
+#pragma unroll
+        for (int p = 0; p < 2; ++p) {
+          const int v = lane + kWave * p;
+          if (v >= f_vc0) {
+            vx[p] = f_x0 + (v - f_vc0);
+            vy[p] = f_y;
+            vz[p] = f_z;
+            fox[p] = f_ox;
+          }
+        }
+      }
+      const int np = NC > kWave ? 2 : 1;
 #pragma unroll
       for (int p = 0; p < 2; ++p) {
         const int v = lane + kWave * p;
-        if (v >= f_vc0) {
-          V.vx[p] = f_x0 + (v - f_vc0);
-          V.vy[p] = f_y;
-          V.vz[p] = f_z;
-          V.fox[p] = f_ox;
+        // the f64 cell centre k_bin_fine measured the SRec offsets from
+        dxc[p] = (float)((G.o[0] + (vx[p] + 0.5) * G.e[0]) - fox[p]);
+        if (p < np) {  // wave-uniform
+          // every load issued unconditionally (cells off the grid read
+          // tstart[0] and are zeroed after): a per-element condition makes
+          // hipcc branch around each load and wait for it
+          bool ok[9];
+#pragma unroll
+          for (int r = 0; r < 9; ++r) {
+            const int yy = vy[p] + (r % 3) - 1, zz = vz[p] + (r / 3) - 1;
+            ok[r] = v < NC && yy >= 0 && yy < g1 && zz >= 0 && zz < g2;
+            const int base = ok[r] ? (zz * g1 + yy) * g0 : 0;
+            st[p][r] = tstart[ok[r] ? base + min(max(vx[p], 0), g0) : 0];
+            en[p][r] = tstart[ok[r] ? base + min(max(vx[p] + 1, 0), g0) : 0];
+          }
+#pragma unroll
+          for (int r = 0; r < 9; ++r) {
+            st[p][r] = ok[r] ? st[p][r] : 0;
+            en[p][r] = ok[r] ? en[p][r] : 0;
+          }
+        } else {
+#pragma unroll
+          for (int r = 0; r < 9; ++r) st[p][r] = en[p][r] = 0;
+        }
+#pragma unroll
+        for (int r = 0; r < 9; ++r) cs[p] += en[p][r] - st[p][r];
+      }
+      const int inc0 = wave_scan_add(cs[0]);
+      const int tot0 = rdlane(inc0, kWave - 1);
+      const int inc1 = np > 1 ? wave_scan_add(cs[1]) + tot0 : tot0;
+      total = rdlane(inc1, kWave - 1);
+      const int ex[2] = {inc0 - cs[0], inc1 - cs[1]};
+#pragma unroll
+      for (int p = 0; p < 2; ++p) {
+        int a = ex[p];
+#pragma unroll
+        for (int r = 0; r < 9; ++r) {
+          cbr[p][r] = a - st[p][r];
+          a += en[p][r] - st[p][r];
+        }
+        colst[lane + kWave * p] = ex[p];
+      }
+      if (lane == 0) colst[kWCols] = total;
+    }
+    wave_sync_mem();
+    NV_STAMP(r1);
+    NV_ACC(2, r0, r1);
+    if (total > kWRec) {
+      // the lane prefix whose blocks end within the budget (slot ends ascend)
+      const bool inr = in && lane < lb;
+      const int endslot = inr ? colst[vcq + S + 1] : 0x7fffffff;
+      const int lb2 = la + __popcll(__ballot(inr && endslot <= kWRec));
+      if (lb2 == la) {
+        // the first lane's block alone exceeds the budget: it and every lane
+        // of its cell go to k_knn_slow from an infinite bound
+        const int vq0 = rdlane(vcq, la);
+        const bool same = inr && vcq == vq0;
+        if (same) {
+          push_slow(L_, qi, INFINITY);
+          atomicAdd(L_.n_unstaged, 1);
+        }
+        la += __popcll(__ballot(same));
+        wave_sync_mem();  // colst is rewritten by the next round
+        continue;
+      }
+      lb = lb2;
+      NC = rdlane(cum, lb - 1);
+      fb &= lb >= kWave ? ~0ull : ((1ull << lb) - 1);
+    }
+    // ---- each segment's row pieces: the starts at its first column, the
+    // ends at its last (the round's cut included), from the tables
+    {
+      int si = 0;
+      for (unsigned long long b = fb; b; b &= b - 1, ++si) {
+        const int f = (int)__builtin_ctzll(b);
+        const int lsl = min(rdlane(sl, f), lb - 1);
+        const int vc0 = rdlane(pre, f), vlast = rdlane(cum, lsl) - 1;
+#pragma unroll
+        for (int p = 0; p < 2; ++p) {
+          const int v = lane + kWave * p;
+#pragma unroll
+          for (int r = 0; r < 9; ++r) {
+            if (v == vc0) sbnd[si][r][0] = st[p][r];
+            if (v == vlast) sbnd[si][r][1] = en[p][r];
+          }
         }
       }
     }
-    return V;
-  };
-  // the 9 rows' record starts st and ends en of every virtual column: every
-  // load issued unconditionally (cells off the grid read tstart[0] and are
-  // zeroed when used): a per-element condition makes hipcc branch around each
-  // load and wait for it
-  auto tload = [&](const Plan &P, const Cols &V, int (&st)[2][9], int (&en)[2][9], int p0,
-                   int p1) {
+    wave_sync_mem();
+#ifdef NAVGPU_KNNW_CHECK
+    for (int q = lane; q < kWRec; q += kWave) spair[kWZg + (q >> 1) * 4 + 2 + (q & 1)] = __int_as_float(-1);
+    wave_sync_mem();
+#endif
+    // ---- staging: per segment, its 9 row pieces as SRec (16 B: f32 offset
+    // from the record's cell centre + x cell); every load of a segment in
+    // flight before any is used; slot from cbr, x shift from dxc (the
+    // record's column's lane), y and z shifts per row. TWO: the round has
+    // columns past 64 (the second table of each lane), a separate copy so
+    // the usual one-table round shuffles only once per value.
+    auto stage = [&](auto TWO) {
+      int si = 0;
+      for (unsigned long long b = fb; b; b &= b - 1, ++si) {
+        const int f = (int)__builtin_ctzll(b);
+        const int lsl = min(rdlane(sl, f), lb - 1);
+        const int vc0 = rdlane(pre, f), vlast = rdlane(cum, lsl) - 1;
+        const int sxf = rdlane(qx, f), sy = rdlane(qy, f), sz = rdlane(qz, f);
+        const WFrame F = wframe(G, sxf, rdlane(qx, min(rdlane(sl, f), lbc - 1)), sy, sz);
+        const int x0 = sxf - S;
+        const int tlast = max(ntg - 1, 0);  // (srec holds at least one record)
+        constexpr int U = NAVGPU_KNNW_U;
+        int glo[9], nr[9];
 #pragma unroll
-    for (int p = 0; p < 2; ++p)
+        for (int r = 0; r < 9; ++r) {  // wave-uniform: scalar registers
+          glo[r] = __builtin_amdgcn_readfirstlane(sbnd[si][r][0]);
+          nr[r] = __builtin_amdgcn_readfirstlane(sbnd[si][r][1]) - glo[r];
+        }
+        for (int k0 = 0;; k0 += U * kWave) {
+          SRec v[9][U];
+          bool more = false;
+          // every load is issued, unconditionally, from a position clamped
+          // into the cloud (a per-element condition makes hipcc branch around
+          // each load and wait for it: nine serial round trips); lanes past a
+          // row piece discard theirs below. (The clamp also keeps a logic
+          // error from reading past the cloud, which would fault the device.)
 #pragma unroll
-      for (int r = 0; r < 9; ++r) {
-        if (p < p0 || p >= p1) continue;
-        const int v = lane + kWave * p;
-        const int yy = V.vy[p] + (r % 3) - 1, zz = V.vz[p] + (r / 3) - 1;
-        const bool ok = (p == 0 || P.NC > kWave) && v < P.NC && yy >= 0 && yy < g1 && zz >= 0 &&
-                        zz < g2;
-        const int base = ok ? (zz * g1 + yy) * g0 : 0;
-        st[p][r] = tstart[ok ? base + min(max(V.vx[p], 0), g0) : 0];
-        en[p][r] = tstart[ok ? base + min(max(V.vx[p] + 1, 0), g0) : 0];
-      }
-  };
-  auto tmask = [&](const Plan &P, const Cols &V, int (&st)[2][9], int (&en)[2][9]) {
+          for (int r = 0; r < 9; ++r)
 #pragma unroll
-    for (int p = 0; p < 2; ++p)
-#pragma unroll
-      for (int r = 0; r < 9; ++r) {
-        const int v = lane + kWave * p;
-        const int yy = V.vy[p] + (r % 3) - 1, zz = V.vz[p] + (r / 3) - 1;
-        const bool ok = (p == 0 || P.NC > kWave) && v < P.NC && yy >= 0 && yy < g1 && zz >= 0 &&
-                        zz < g2;
-        st[p][r] = ok ? st[p][r] : 0;
-        en[p][r] = ok ? en[p][r] : 0;
-      }
-  };
-  // ---- the first chunk, then one per iteration; the next chunk's query
-  // loads and round-0 table loads are issued during this chunk's scan and
-  // land during its exact stage
-  int chunk = resolve(draw());
-  if (chunk < 0) return;
-  int q_idx, q_cell;
-  {
-    const int qi = min(chunk * kWave + lane, nq - 1);
-    q_idx = QS.idx[qi];
-    q_cell = QS.cell[qi];
-  }
-  double q_x, q_y, q_z;
-  {
-    const double *pp = QS.pts + 3 * (size_t)q_idx;
-    q_x = pp[0];
-    q_y = pp[1];
-    q_z = pp[2];
-  }
-  // the next chunk's first-round tables (its first 64 columns), loaded during
-  // this chunk's exact stage (pref: they are)
-  int pst[9], pen[9];
-  bool pref = false;
-  while (true) {
-    NV_ACC(1, 0ull, 1ull);
-    const int tn = draw();  // the next chunk's ticket, resolved after the staging
-    const Cells C = cells_of(chunk, q_cell);
-    const int qi = chunk * kWave + lane;
-    int cn = -1, n_idx = 0, n_cell = 0;
-    double n_x = 0.0, n_y = 0.0, n_z = 0.0;
-    // the hooks below run in the chunk's last round, once it is past its
-    // staging (or after the rounds, if that round ended early)
-    bool hookA = false, hookB = false;
-    auto next_positions = [&]() {
-      hookA = true;
-      cn = resolve(tn);
-      if (cn >= 0) {
-        const int qn = min(cn * kWave + lane, nq - 1);
-        n_idx = QS.idx[qn];
-        n_cell = QS.cell[qn];
-      }
-    };
-    auto next_tables = [&]() {
-      hookB = true;
-      if (cn < 0) return;
-      const double *pp = QS.pts + 3 * (size_t)n_idx;
-      n_x = pp[0];
-      n_y = pp[1];
-      n_z = pp[2];
-      const Cells Cn = cells_of(cn, n_cell);
-      const Plan Pn = plan_of(Cn, 0);
-      int tst[2][9], ten[2][9];
-      tload(Pn, cols_of(Cn, Pn), tst, ten, 0, 1);  // the first table (64 columns) only
-#pragma unroll
-      for (int r = 0; r < 9; ++r) {
-        pst[r] = tst[0][r];
-        pen[r] = ten[0][r];
-      }
-    };
-    for (int la = 0; la < C.nlive;) {
-      NV_STAMP(r0);
-      NV_ACC(7, 0ull, 1ull);
-      const Plan P0 = plan_of(C, la);
-      const int lbc = P0.lb;  // the frames use the column-fit round (a budget cut keeps them)
-      int lb = P0.lb, NC = P0.NC;
-      unsigned long long fb = P0.fb;
-      const bool in = P0.in;
-      const int sl = P0.sl, pre = P0.pre, vcq = P0.vcq, cum = P0.cum, xf = P0.xf;
-      const Cols V = cols_of(C, P0);
-      // ---- column tables: cs = the column's records (its 9 rows'),
-      // cbr[p][r] + g = the slot of the record at cell-sorted position g of
-      // row r; dxc = the column's cell centre in its segment's frame (x)
-      int cbr[2][9], st[2][9], en[2][9];
-      float dxc[2];
-      int total;
-      {
-        if (la == 0 && pref) {
+            for (int u = 0; u < U; ++u) {
+              const int k = k0 + u * kWave + lane;
+#ifdef NAVGPU_KNNW_CHECK
+              if (k < nr[r] && (glo[r] + k < 0 || glo[r] + k >= ntg))
+                printf("knnw chunk %d lane %d seg %d row %d: srec %d of %d (glo %d nr %d)\n",
+                       chunk, lane, si, r, glo[r] + k, ntg, glo[r], nr[r]);
+#endif
+              // (a wave-uniform row base and a 32-bit lane offset)
+              v[r][u] = (srec + glo[r])[min(k, tlast - glo[r])];
+            }
 #pragma unroll
           for (int r = 0; r < 9; ++r) {
-            st[0][r] = pst[r];
-            en[0][r] = pen[r];
-          }
-          tload(P0, V, st, en, 1, 2);  // (loads nothing unless NC > 64)
-        } else {
-          tload(P0, V, st, en, 0, 2);
-        }
-        pref = false;
-        tmask(P0, V, st, en);
-        int cs[2] = {0, 0};
+            more |= k0 + U * kWave < nr[r];
+            const int yy = sy + (r % 3) - 1, zz = sz + (r / 3) - 1;
+            const float dy = (float)((G.o[1] + (yy + 0.5) * G.e[1]) - F.o[1]);
+            const float dz = (float)((G.o[2] + (zz + 0.5) * G.e[2]) - F.o[2]);
 #pragma unroll
-        for (int p = 0; p < 2; ++p) {
-          // the f64 cell centre k_bin_fine measured the SRec offsets from
-          dxc[p] = (float)((G.o[0] + (V.vx[p] + 0.5) * G.e[0]) - V.fox[p]);
-#pragma unroll
-          for (int r = 0; r < 9; ++r) cs[p] += en[p][r] - st[p][r];
-        }
-        const int np = NC > kWave ? 2 : 1;
-        const int inc0 = wave_scan_add(cs[0]);
-        const int tot0 = rdlane(inc0, kWave - 1);
-        const int inc1 = np > 1 ? wave_scan_add(cs[1]) + tot0 : tot0;
-        total = rdlane(inc1, kWave - 1);
-        const int ex[2] = {inc0 - cs[0], inc1 - cs[1]};
-#pragma unroll
-        for (int p = 0; p < 2; ++p) {
-          int a = ex[p];
-#pragma unroll
-          for (int r = 0; r < 9; ++r) {
-            cbr[p][r] = a - st[p][r];
-            a += en[p][r] - st[p][r];
-          }
-          colst[lane + kWave * p] = ex[p];
-        }
-        if (lane == 0) colst[kWCols] = total;
-      }
-      wave_sync_mem();
-      NV_STAMP(r1);
-      NV_ACC(2, r0, r1);
-      if (total > kWRec) {
-        // the lane prefix whose blocks end within the budget (slot ends ascend)
-        const bool inr = in && lane < lb;
-        const int endslot = inr ? colst[vcq + S + 1] : 0x7fffffff;
-        const int lb2 = la + __popcll(__ballot(inr && endslot <= kWRec));
-        if (lb2 == la) {
-          // the first lane's block alone exceeds the budget: it and every
-          // lane of its cell go to k_knn_slow from an infinite bound
-          const int vq0 = rdlane(vcq, la);
-          const bool same = inr && vcq == vq0;
-          if (same) {
-            push_slow(L_, qi, INFINITY);
-            atomicAdd(L_.n_unstaged, 1);
-          }
-          la += __popcll(__ballot(same));
-          wave_sync_mem();  // colst is rewritten by the next round
-          continue;
-        }
-        lb = lb2;
-        NC = rdlane(cum, lb - 1);
-        fb &= lb >= kWave ? ~0ull : ((1ull << lb) - 1);
-      }
-      // ---- each segment's row pieces: the starts at its first column, the
-      // ends at its last (the round's cut included), from the tables
-      {
-        int si = 0;
-        for (unsigned long long b = fb; b; b &= b - 1, ++si) {
-          const int f = (int)__builtin_ctzll(b);
-          const int lsl = min(rdlane(sl, f), lb - 1);
-          const int vc0 = rdlane(pre, f), vlast = rdlane(cum, lsl) - 1;
-#pragma unroll
-          for (int p = 0; p < 2; ++p) {
-            const int v = lane + kWave * p;
-#pragma unroll
-            for (int r = 0; r < 9; ++r) {
-              if (v == vc0) sbnd[si][r][0] = st[p][r];
-              if (v == vlast) sbnd[si][r][1] = en[p][r];
-            }
-          }
-        }
-      }
-      wave_sync_mem();
-      // ---- staging: per segment, its 9 row pieces as SRec (16 B: f32 offset
-      // from the record's cell centre + x cell); every load of a segment in
-      // flight before any is used; slot from cbr, x shift from dxc (the
-      // record's column's lane), y and z shifts per row. TWO: the round has
-      // columns past 64 (the second table of each lane), a separate copy so
-      // the usual one-table round shuffles only once per value.
-      auto stage = [&](auto TWO) {
-        int si = 0;
-        for (unsigned long long b = fb; b; b &= b - 1, ++si) {
-          const int f = (int)__builtin_ctzll(b);
-          const int lsl = min(rdlane(sl, f), lb - 1);
-          const int vc0 = rdlane(pre, f), vlast = rdlane(cum, lsl) - 1;
-          const int sxf = rdlane(C.qx, f), sy = rdlane(C.qy, f), sz = rdlane(C.qz, f);
-          const WFrame F = wframe(G, sxf, rdlane(C.qx, min(rdlane(sl, f), lbc - 1)), sy, sz);
-          const int x0c = sxf - S;
-          const int tlast = max(ntg - 1, 0);  // (srec holds at least one record)
-          constexpr int U = NAVGPU_KNNW_U;
-          int glo[9], nr[9];
-#pragma unroll
-          for (int r = 0; r < 9; ++r) {  // wave-uniform: scalar registers
-            glo[r] = __builtin_amdgcn_readfirstlane(sbnd[si][r][0]);
-            nr[r] = __builtin_amdgcn_readfirstlane(sbnd[si][r][1]) - glo[r];
-          }
-          for (int k0 = 0;; k0 += U * kWave) {
-            SRec v[9][U];
-            bool more = false;
-            // every load is issued, unconditionally, from a position clamped
-            // into the cloud (a per-element condition makes hipcc branch
-            // around each load and wait for it: nine serial round trips);
-            // lanes past a row piece discard theirs below. (The clamp also
-            // keeps a logic error from reading past the cloud, which would
-            // fault the device.)
-#pragma unroll
-            for (int r = 0; r < 9; ++r)
-#pragma unroll
-              for (int u = 0; u < U; ++u) {
-                const int k = k0 + u * kWave + lane;
-                // (a wave-uniform row base and a 32-bit lane offset)
-                v[r][u] = (srec + glo[r])[min(k, tlast - glo[r])];
+            for (int u = 0; u < U; ++u) {
+              const int k = k0 + u * kWave + lane;
+              const int vcol = vc0 + v[r][u].cx - x0;
+              const int il = vcol & (kWave - 1);
+              int cb = __shfl(cbr[0][r], il, kWave);
+              float dx = __shfl(dxc[0], il, kWave);
+              if constexpr (decltype(TWO)::value) {
+                const int c1 = __shfl(cbr[1][r], il, kWave);
+                const float d1 = __shfl(dxc[1], il, kWave);
+                cb = vcol >= kWave ? c1 : cb;
+                dx = vcol >= kWave ? d1 : dx;
               }
-#pragma unroll
-            for (int r = 0; r < 9; ++r) {
-              more |= k0 + U * kWave < nr[r];
-              const int yy = sy + (r % 3) - 1, zz = sz + (r / 3) - 1;
-              const float dy = (float)((G.o[1] + (yy + 0.5) * G.e[1]) - F.o[1]);
-              const float dz = (float)((G.o[2] + (zz + 0.5) * G.e[2]) - F.o[2]);
-#pragma unroll
-              for (int u = 0; u < U; ++u) {
-                const int k = k0 + u * kWave + lane;
-                const int vcol = vc0 + v[r][u].cx - x0c;
-                const int il = vcol & (kWave - 1);
-                int cb = __shfl(cbr[0][r], il, kWave);
-                float dx = __shfl(dxc[0], il, kWave);
-                if constexpr (decltype(TWO)::value) {
-                  const int c1 = __shfl(cbr[1][r], il, kWave);
-                  const float d1 = __shfl(dxc[1], il, kWave);
-                  cb = vcol >= kWave ? c1 : cb;
-                  dx = vcol >= kWave ? d1 : dx;
-                }
-                if (k < nr[r] && vcol <= vlast) {
-                  const int slot = cb + glo[r] + k;
-                  float *d = spair + (slot >> 1) * 4 + (slot & 1);
-                  d[0] = v[r][u].x + dx;
-                  d[2] = v[r][u].y + dy;
-                  d[kWZg] = v[r][u].z + dz;
-                  d[kWZg + 2] = __int_as_float(glo[r] + k);
-                }
+              if (k < nr[r] && vcol <= vlast) {
+                const int slot = cb + glo[r] + k;
+                float *d = spair + (slot >> 1) * 4 + (slot & 1);
+                d[0] = v[r][u].x + dx;
+                d[2] = v[r][u].y + dy;
+                d[kWZg] = v[r][u].z + dz;
+                d[kWZg + 2] = __int_as_float(glo[r] + k);
               }
             }
-            if (!more) break;  // wave-uniform: nr and k0 are
           }
+          if (!more) break;  // wave-uniform: nr and k0 are
         }
-      };
-      if (NC > kWave)
-        stage(std::true_type{});
-      else
-        stage(std::false_type{});
-      wave_sync_mem();
-      NV_STAMP(r2);
-      NV_ACC(3, r1, r2);
-      // ---- the next chunk: its ticket, then its query positions' loads
-      // (they land during the scan)
-      const bool lastround = lb >= C.nlive;
-      if (lastround) next_positions();
-      // the last query cell of the lane's segment in the column-fit round (its frame)
-      const int xl = __shfl(C.qx, min(sl, lbc - 1), kWave);
-      // ---- the round's queries, one per lane: the scan (k_knn's) of the
-      // lane's block [t0, t1)
-      const bool act = in && lane < lb;
-      const double qv[3] = {q_x, q_y, q_z};
+      }
+    };
+    if (NC > kWave)
+      stage(std::true_type{});
+    else
+      stage(std::false_type{});
+    wave_sync_mem();
+    NV_STAMP(r2);
+    NV_ACC(3, r1, r2);
+    // the last query cell of the lane's segment in the column-fit round (its frame)
+    const int xl = __shfl(qx, min(sl, lbc - 1), kWave);
+#ifdef NAVGPU_KNNW_CHECK
+    if (in && lane < lb) {
+      const int t0 = colst[vcq - S], t1 = colst[vcq + S + 1];
+      int bad = -1;
+      for (int q = t0; q < t1; ++q)
+        if (__float_as_int(spair[kWZg + (q >> 1) * 4 + 2 + (q & 1)]) < 0) bad = q;
+      if (bad >= 0) {
+        printf("CHK chunk %d lane %d la %d lb %d lbc %d NC %d total %d vcq %d sf %d sl %d t0 %d t1 %d bad %d fb %llx qx %d qrow %d\n",
+               chunk, lane, la, lb, lbc, NC, total, vcq, sf, sl, t0, t1, bad, fb, qx, qrow);
+        for (int v = vcq - S; v <= vcq + S + 1; ++v) printf("CHK chunk %d colst[%d] = %d\n", chunk, v, colst[v]);
+      }
+    }
+    {
+      int si2 = 0;
+      for (unsigned long long b = fb; b; b &= b - 1, ++si2) {
+        const int f = (int)__builtin_ctzll(b);
+        const int lsl = min(rdlane(sl, f), lb - 1);
+        if (lane == 0 && (chunk == 5 || chunk == 36 || chunk == 40))
+          printf("SEG chunk %d si %d f %d lsl %d vc0 %d vlast %d x %d..%d row %d | %d %d %d %d %d %d %d %d %d / %d %d %d %d %d %d %d %d %d\n",
+                 chunk, si2, f, lsl, rdlane(pre, f), rdlane(cum, lsl) - 1, rdlane(qx, f), rdlane(qx, lsl), rdlane(qrow, f),
+                 sbnd[si2][0][0], sbnd[si2][1][0], sbnd[si2][2][0], sbnd[si2][3][0], sbnd[si2][4][0], sbnd[si2][5][0], sbnd[si2][6][0], sbnd[si2][7][0], sbnd[si2][8][0],
+                 sbnd[si2][0][1], sbnd[si2][1][1], sbnd[si2][2][1], sbnd[si2][3][1], sbnd[si2][4][1], sbnd[si2][5][1], sbnd[si2][6][1], sbnd[si2][7][1], sbnd[si2][8][1]);
+      }
+    }
+#endif
+    // ---- the round's queries, one per lane (k_knn's scan, exact stage and
+    // certificate on the lane's block [t0, t1))
+    if (in && lane < lb) {
+      const double qv[3] = {Q.x, Q.y, Q.z};
+      const int c[3] = {qx, qy, qz};
+      const int t0 = colst[vcq - S], t1 = colst[vcq + S + 1];
+      const WFrame F = wframe(G, xf, xl, qy, qz);
+      const double qr[3] = {qv[0] - F.o[0], qv[1] - F.o[1], qv[2] - F.o[2]};
+      const double Dq = fmax(F.Dt, fmax(fabs(qr[0]), fmax(fabs(qr[1]), fabs(qr[2]))));
+      // each f32 difference is within dl of the exact one: the staged target
+      // offset s + d carries <= 4 u Dq (s from the cell centre, the centre's
+      // shift d, their sum), the query's u Dq, the subtraction 2 u Dq, with
+      // u = 2^-24 (SRec)
+      const double dl = Dq * 0x1p-21;
+      const f2 qx2 = {(float)qr[0], (float)qr[0]}, qy2 = {(float)qr[1], (float)qr[1]},
+               qz2 = {(float)qr[2], (float)qr[2]};
+      const double Lr = block_reach(G, qv, c, 1);
       uint32_t key[KL];
 #pragma unroll
       for (int s = 0; s < KL; ++s) key[s] = kNoKey;
-      int t0 = 0, t1 = 0, ta = 0;
-      double dl = 0.0, Dq = 0.0;
-      if (act) {
-        t0 = colst[vcq - S];
-        t1 = colst[vcq + S + 1];
-        const WFrame F = wframe(G, xf, xl, C.qy, C.qz);
-        const double qr[3] = {qv[0] - F.o[0], qv[1] - F.o[1], qv[2] - F.o[2]};
-        Dq = fmax(F.Dt, fmax(fabs(qr[0]), fmax(fabs(qr[1]), fabs(qr[2]))));
-        // each f32 difference is within dl of the exact one: the staged
-        // target offset s + d carries <= 4 u Dq (s from the cell centre, the
-        // centre's shift d, their sum), the query's u Dq, the subtraction
-        // 2 u Dq, with u = 2^-24 (SRec)
-        dl = Dq * 0x1p-21;
-        const f2 qx2 = {(float)qr[0], (float)qr[0]}, qy2 = {(float)qr[1], (float)qr[1]},
-                 qz2 = {(float)qr[2], (float)qr[2]};
-        auto ins = [&](uint32_t kk) {  // keep the K+1 smallest keys sorted
+      auto ins = [&](uint32_t kk) {  // keep the K+1 smallest keys sorted
 #pragma unroll
-          for (int s = K; s > 0; --s) key[s] = umed3(key[s - 1], key[s], kk);
-          key[0] = min(key[0], kk);
-        };
-        auto dist2 = [&](const float *p) {  // packed f32 squared distances of a pair
-          const float4 xy = *(const float4 *)p;
-          const float2 zz = *(const float2 *)(p + kWZg);
+        for (int s = K; s > 0; --s) key[s] = umed3(key[s - 1], key[s], kk);
+        key[0] = min(key[0], kk);
+      };
+      auto dist2 = [&](const float *p) {  // packed f32 squared distances of a pair
+        const float4 xy = *(const float4 *)p;
+        const float2 zz = *(const float2 *)(p + kWZg);
+        const f2 fx2 = f2{xy.x, xy.y} - qx2, fy2 = f2{xy.z, xy.w} - qy2,
+                 fz2 = f2{zz.x, zz.y} - qz2;
+        return __builtin_elementwise_fma(fz2, fz2, __builtin_elementwise_fma(fy2, fy2, fx2 * fx2));
+      };
+      const int ta = t0 & ~1;
+      const int npr = (t1 - ta + 1) >> 1;  // pairs the block touches
+      const bool overflow = (t1 - ta) > (1 << kKeyBits);
+      const float *cur = spair + (ta >> 1) * 4;
+      if (npr > 0) {  // first pair: may start before the block (odd t0) or end past it
+        const f2 d = dist2(cur);
+        const uint32_t k0 = knn_key(d[0], vmask, 0u), k1 = knn_key(d[1], vmask, 1u);
+        if (ta >= t0) ins(k0);
+        if (ta + 1 < t1) ins(k1);
+        cur += 4;
+      }
+      if (npr > 2) {  // interior pairs: the key's local id is the wave-uniform pair counter
+        const float *lastp = spair + ((ta >> 1) + npr - 1) * 4;
+        uint32_t v2 = 2;
+        float4 xy = *(const float4 *)cur;
+        float2 zz = *(const float2 *)(cur + kWZg);
+        do {
+          const float4 nxy = *(const float4 *)(cur + 4);
+          const float2 nzz = *(const float2 *)(cur + 4 + kWZg);
           const f2 fx2 = f2{xy.x, xy.y} - qx2, fy2 = f2{xy.z, xy.w} - qy2,
                    fz2 = f2{zz.x, zz.y} - qz2;
-          return __builtin_elementwise_fma(fz2, fz2,
-                                           __builtin_elementwise_fma(fy2, fy2, fx2 * fx2));
-        };
-        ta = t0 & ~1;
-        const int npr = (t1 - ta + 1) >> 1;  // pairs the block touches
-        const float *cur = spair + (ta >> 1) * 4;
-        if (npr > 0) {  // first pair: may start before the block (odd t0) or end past it
-          const f2 d = dist2(cur);
-          const uint32_t k0 = knn_key(d[0], vmask, 0u), k1 = knn_key(d[1], vmask, 1u);
-          if (ta >= t0) ins(k0);
-          if (ta + 1 < t1) ins(k1);
+          const f2 d =
+              __builtin_elementwise_fma(fz2, fz2, __builtin_elementwise_fma(fy2, fy2, fx2 * fx2));
+          ins(knn_key(d[0], vmask, v2));
+          ins(knn_key(d[1], vmask, v2 + 1));
           cur += 4;
-        }
-        if (npr > 2) {  // interior pairs: the key's local id is the wave-uniform pair counter
-          const float *lastp = spair + ((ta >> 1) + npr - 1) * 4;
-          uint32_t v2 = 2;
-          float4 xy = *(const float4 *)cur;
-          float2 zz = *(const float2 *)(cur + kWZg);
-          do {
-            const float4 nxy = *(const float4 *)(cur + 4);
-            const float2 nzz = *(const float2 *)(cur + 4 + kWZg);
-            const f2 fx2 = f2{xy.x, xy.y} - qx2, fy2 = f2{xy.z, xy.w} - qy2,
-                     fz2 = f2{zz.x, zz.y} - qz2;
-            const f2 d = __builtin_elementwise_fma(fz2, fz2,
-                                                   __builtin_elementwise_fma(fy2, fy2, fx2 * fx2));
-            ins(knn_key(d[0], vmask, v2));
-            ins(knn_key(d[1], vmask, v2 + 1));
-            cur += 4;
-            v2 += 2;
-            xy = nxy;
-            zz = nzz;
-          } while (cur < lastp);
-        }
-        if (npr > 1) {  // last pair: may end past the block
-          const f2 d = dist2(cur);
-          const uint32_t lid = (uint32_t)(2 * (npr - 1)) & kKeyMask;
-          const uint32_t k0 = (__float_as_uint(d[0]) & vmask) | lid;
-          const uint32_t k1 = (__float_as_uint(d[1]) & vmask) | (lid + 1);
-          ins(k0);
-          if (ta + 2 * (npr - 1) + 1 < t1) ins(k1);
-        }
+          v2 += 2;
+          xy = nxy;
+          zz = nzz;
+        } while (cur < lastp);
+      }
+      if (npr > 1) {  // last pair: may end past the block
+        const f2 d = dist2(cur);
+        const uint32_t lid = (uint32_t)(2 * (npr - 1)) & kKeyMask;
+        const uint32_t k0 = (__float_as_uint(d[0]) & vmask) | lid;
+        const uint32_t k1 = (__float_as_uint(d[1]) & vmask) | (lid + 1);
+        ins(k0);
+        if (ta + 2 * (npr - 1) + 1 < t1) ins(k1);
       }
       NV_STAMP(r3);
       NV_ACC(4, r2, r3);
-      // ---- the next chunk's coordinates and round-0 tables, in flight
-      // during this chunk's exact stage
-      if (lastround) next_tables();
-      NV_STAMP(r4);
-      NV_ACC(6, r3, r4);
-      // ---- exact f64 stage on the K best keys and the certificate (k_knn's)
-      if (act) {
-        const int c[3] = {C.qx, C.qy, C.qz};
-        const double Lr = block_reach(G, qv, c, 1);
-        const bool overflow = (t1 - ta) > (1 << kKeyBits);
-        bool ok = !overflow && Dq < 1e17;
-        double ed[K];
-        int ei[K];
-        if (key[0] != kNoKey) {
-          int gpos[K];
+      bool ok = !overflow && Dq < 1e17;
+      // exact f64 stage on the K best keys (as in k_knn)
+      double ed[K];
+      int ei[K];
+      if (key[0] != kNoKey) {
+        int gpos[K];
 #pragma unroll
-          for (int s = 0; s < K; ++s) {
-            const uint32_t kk = key[s] != kNoKey ? key[s] : key[0];
-            const int p = min(max(ta + (int)(kk & kKeyMask), t0), max(t1 - 1, t0));
-            gpos[s] = __float_as_int(spair[kWZg + (p >> 1) * 4 + 2 + (p & 1)]);
-          }
-          // all 2 K gathers in flight before any is used (the scheduler would
-          // otherwise sink each pair to its use: a chain of round trips)
-          // (x, y) as 16 B and (z, index) as 12 B: 7 registers per record
-          double2 gxy[K];
-          int3 gzi[K];
+        for (int s = 0; s < K; ++s) {
+          const uint32_t kk = key[s] != kNoKey ? key[s] : key[0];
+          const int p = min(max(ta + (int)(kk & kKeyMask), t0), max(t1 - 1, t0));
+          gpos[s] = __float_as_int(spair[kWZg + (p >> 1) * 4 + 2 + (p & 1)]);
+        }
+        // all 2 K gathers in flight before any is used (the scheduler would
+        // otherwise sink each pair to its use: a chain of round trips)
+        double2 gxy[K], gzi[K];
 #pragma unroll
-          for (int s = 0; s < K; ++s) {
-            gpos[s] = min(max(gpos[s], 0), max(ntg - 1, 0));  // (as the staging clamp)
-            const PRec *tp = tsort + gpos[s];
-            gxy[s] = *(const double2 *)&tp->x;
-            gzi[s] = *(const int3 *)&tp->z;
-          }
-          __builtin_amdgcn_sched_barrier(0);
+        for (int s = 0; s < K; ++s) {
+#ifdef NAVGPU_KNNW_CHECK
+          if (gpos[s] < 0 || gpos[s] >= ntg)
+            printf("knnw chunk %d lane %d: gpos %d of %d (key %x t0 %d t1 %d)\n", chunk, lane,
+                   gpos[s], ntg, key[s], t0, t1);
+#endif
+          gpos[s] = min(max(gpos[s], 0), max(ntg - 1, 0));  // (as the staging clamp above)
+          const PRec *tp = tsort + gpos[s];
+          gxy[s] = *(const double2 *)&tp->x;
+          gzi[s] = *(const double2 *)&tp->z;
+        }
+        __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-          for (int s = 0; s < K; ++s) {
-            const bool val = key[s] != kNoKey;
-            const double2 xy = gxy[s];
-            const double pz = __hiloint2double(gzi[s].y, gzi[s].x);
-            const int pid = gzi[s].z;
-            const double ddx = xy.x - qv[0], ddy = xy.y - qv[1], ddz = pz - qv[2];
-            const double dsq = ddx * ddx + ddy * ddy + ddz * ddz;  // utils/kdtree.c:16
-            ei[s] = val ? pid : -1;
-            ed[s] = val ? __builtin_sqrt(dsq) : INFINITY;
-            if (val && !(ed[s] < INFINITY)) {  // an inf/NaN distance is never a neighbour (kdtree.c:117)
-              ed[s] = INFINITY;
-              ei[s] = -1;
-              ok = false;
-            }
-          }
-        } else {
-#pragma unroll
-          for (int s = 0; s < K; ++s) {
+        for (int s = 0; s < K; ++s) {
+          const bool val = key[s] != kNoKey;
+          const double2 xy = gxy[s], zi = gzi[s];
+          const double pz = zi.x;
+          const int pid = __double2loint(zi.y);
+          const double ddx = xy.x - qv[0], ddy = xy.y - qv[1], ddz = pz - qv[2];
+          const double dsq = ddx * ddx + ddy * ddy + ddz * ddz;  // utils/kdtree.c:16
+          ei[s] = val ? pid : -1;
+          ed[s] = val ? __builtin_sqrt(dsq) : INFINITY;
+          if (val && !(ed[s] < INFINITY)) {  // an inf/NaN distance is never a neighbour (kdtree.c:117)
             ed[s] = INFINITY;
             ei[s] = -1;
+            ok = false;
           }
         }
-        // certificate bound on every candidate left out
-        double B = INFINITY;
-        if (Lr < INFINITY) {
-          const double Lg = Lr - 2.0 * G.delta;
-          B = Lg > 0.0 ? Lg * Lg : 0.0;
-        }
-        if (key[K] != kNoKey) {
-          const double Vk = (double)__uint_as_float(key[K] & vmask);
-          B = fmin(B, Vk - f32_err(Vk, dl));
-        }
-        bool sorted = true;
+      } else {
 #pragma unroll
-        for (int s = 1; s < K; ++s) sorted &= !knn_less_bf(ed[s], ei[s], ed[s - 1], ei[s - 1]);
-        for (int pass = 0; pass < K - 1 && __any(!sorted); ++pass) {
-#pragma unroll
-          for (int u = 1; u < K; ++u) knn_cx(ed[u - 1], ei[u - 1], ed[u], ei[u]);
-          sorted = true;
-#pragma unroll
-          for (int s = 1; s < K; ++s) sorted &= !knn_less_bf(ed[s], ei[s], ed[s - 1], ei[s - 1]);
-        }
-        const double dk = ed[K - 1];
-        const double dk2 = dk * dk;
-        if (dk < INFINITY)
-          ok = ok && B > dk2 * (1.0 + 0x1p-46);
-        else
-          ok = ok && B == INFINITY;
-        if (ok) {
-          const size_t q = (size_t)q_idx;
-          if (K % 4 == 0 && L_.vec_out) {
-#pragma unroll
-            for (int s = 0; s < K; s += 4)
-              *(int4 *)(oidx + q * K + s) = make_int4(ei[s], ei[s + 1], ei[s + 2], ei[s + 3]);
-#pragma unroll
-            for (int s = 0; s < K; s += 2)
-              *(double2 *)(odist + q * K + s) = make_double2(ed[s], ed[s + 1]);
-          } else {
-#pragma unroll
-            for (int s = 0; s < K; ++s) {
-              oidx[q * K + s] = ei[s];
-              odist[q * K + s] = ed[s];
-            }
-          }
-        } else {
-          push_slow(L_, qi, (dk < INFINITY && !overflow) ? dk2 * (1.0 + 0x1p-46) : INFINITY);
+        for (int s = 0; s < K; ++s) {
+          ed[s] = INFINITY;
+          ei[s] = -1;
         }
       }
-      NV_STAMP(r5);
-      NV_ACC(5, r4, r5);
-      la = lb;
-      wave_sync_mem();  // LDS is restaged by the next round
+      // certificate bound on every candidate left out
+      double B = INFINITY;
+      if (Lr < INFINITY) {
+        const double Lg = Lr - 2.0 * G.delta;
+        B = Lg > 0.0 ? Lg * Lg : 0.0;
+      }
+      if (key[K] != kNoKey) {
+        const double V = (double)__uint_as_float(key[K] & vmask);
+        B = fmin(B, V - f32_err(V, dl));
+      }
+      bool sorted = true;
+#pragma unroll
+      for (int s = 1; s < K; ++s) sorted &= !knn_less_bf(ed[s], ei[s], ed[s - 1], ei[s - 1]);
+      for (int pass = 0; pass < K - 1 && __any(!sorted); ++pass) {
+#pragma unroll
+        for (int u = 1; u < K; ++u) knn_cx(ed[u - 1], ei[u - 1], ed[u], ei[u]);
+        sorted = true;
+#pragma unroll
+        for (int s = 1; s < K; ++s) sorted &= !knn_less_bf(ed[s], ei[s], ed[s - 1], ei[s - 1]);
+      }
+      const double dk = ed[K - 1];
+      const double dk2 = dk * dk;
+      if (dk < INFINITY)
+        ok = ok && B > dk2 * (1.0 + 0x1p-46);
+      else
+        ok = ok && B == INFINITY;
+      if (ok) {
+        const size_t q = (size_t)Q.idx;
+        if (K % 4 == 0 && L_.vec_out) {
+#pragma unroll
+          for (int s = 0; s < K; s += 4)
+            *(int4 *)(oidx + q * K + s) = make_int4(ei[s], ei[s + 1], ei[s + 2], ei[s + 3]);
+#pragma unroll
+          for (int s = 0; s < K; s += 2)
+            *(double2 *)(odist + q * K + s) = make_double2(ed[s], ed[s + 1]);
+        } else {
+#pragma unroll
+          for (int s = 0; s < K; ++s) {
+            oidx[q * K + s] = ei[s];
+            odist[q * K + s] = ed[s];
+          }
+        }
+      } else {
+        push_slow(L_, qi, (dk < INFINITY && !overflow) ? dk2 * (1.0 + 0x1p-46) : INFINITY);
+      }
+      NV_STAMP(r4);
+      NV_ACC(5, r3, r4);
     }
-    if (!hookA) next_positions();
-    if (!hookB) next_tables();
-    if (cn < 0) break;
-    chunk = cn;
-    q_idx = n_idx;
-    q_cell = n_cell;
-    q_x = n_x;
-    q_y = n_y;
-    q_z = n_z;
-    pref = true;
+    NV_STAMP(r5);
+    NV_ACC(6, r2, r5);
+    la = lb;
+    wave_sync_mem();  // LDS is restaged by the next round
   }
   NV_STAMP(w9);
   NV_ACC(8, w0, w9);
-  NV_WFLUSH((int)(blockIdx.x * kWPB) + wid);
+  NV_WFLUSH(chunk);
 }
 
 // ============================================================ k_knn_slow
@@ -2131,27 +2023,6 @@ int knn_stamps_take(unsigned long long *out16) {
 }
 }  // namespace nv
 
-// k_knnw's persistent grid: the workgroups resident at once (the occupancy
-// API's count per CU times the CUs), a multiple of 8 (the XCD pools), never
-// more than the chunks need; NAVGPU_KNN_BLOCKS overrides (workgroups per XCD)
-template <int K>
-static int knnw_grid(navgpu_ctx *ctx, int nchunk) {
-  static int occ = 0, ncu = 0;
-  if (!occ) {
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_knnw<K>, kWave * kWPB, 0) !=
-            hipSuccess ||
-        occ < 1)
-      occ = 1;
-    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, ctx->device) !=
-            hipSuccess ||
-        ncu < 1)
-      ncu = 8;
-  }
-  const int need = 8 * (((nchunk + 7) / 8 + kWPB - 1) / kWPB);
-  const int res = ctx->knn_blocks > 0 ? 8 * ctx->knn_blocks : std::max(8, ncu * occ / 8 * 8);
-  return std::min(need, res);
-}
-
 // The k-NN call (navgpu_knn_dev): index build, query pass, slow pass; all on
 // the context's stream, nothing allocated once the workspace is warm.
 static int knn_run(navgpu_ctx *ctx, const double *tgt, size_t nt, const double *queries,
@@ -2289,19 +2160,17 @@ static int knn_run(navgpu_ctx *ctx, const double *tgt, size_t nt, const double *
   const dim3 g(8 * nbx), b(kTileThreads);
   const dim3 gs(std::max<unsigned>(1, std::min<unsigned>(2048, grid1d(nq, 256))));
   const float lambda = (float)ctx->knn_lambda;
-  // k_knnw: persistent waves, as many as are resident at once (more would
-  // only start when others finish), each drawing chunks of 64 cell-sorted
-  // queries from its XCD's pool (counters + 4: the tickets)
+  // k_knnw: one 64-lane block per chunk of 64 cell-sorted queries, chunks
+  // dealt to the XCDs in contiguous ranges
   const int nchunk = (int)((nq + kWave - 1) / kWave);
-  const dim3 bw(kWave * kWPB);
+  const dim3 gw(8 * ((nchunk + 7) / 8)), bw(kWave);
   const bool waves = ctx->knn_mode == 1;
   const QSide QS{queries, qperm, qcell};
 #define KNN_CASE(KK)                                                                        \
   case KK:                                                                                  \
     if (waves)                                                                              \
-      hipLaunchKernelGGL((k_knnw<KK>), dim3(knnw_grid<KK>(ctx, nchunk)), bw, 0, s, gp, tstart,   \
-                         tsort, srec, QS, (int)nq, (int)nt,                                 \
-                         idx, dist, lists, counters + 4);                                   \
+      hipLaunchKernelGGL((k_knnw<KK>), gw, bw, 0, s, gp, tstart, tsort, srec, QS, (int)nq,      \
+                         (int)nt, idx, dist, lists);                                        \
     else                                                                                    \
       hipLaunchKernelGGL((k_knn<KK>), g, b, 0, s, gp, tstart, tsort, qstart, QS,   \
                          idx, dist, lists, lambda);                                         \

@@ -389,7 +389,7 @@ __device__ void block_nth_element(const double *key, IdxT *P, IdxT *T, int first
       int c = lane < nw ? bcn[b][lane] : 0;
       int incl = c;
 #pragma unroll
-      for (int o = 1; o < NWM; o <<= 1) {
+      for (int o = 1; o <= NWM; o <<= 1) {  // lanes 0 .. NWM: up to 17 terms
         const int t = __shfl_up(incl, o, kWave);
         if (lane >= o) incl += t;
       }
@@ -830,7 +830,10 @@ __global__ __launch_bounds__(kRowsBlock) void k_rows_match(
   if (tie && !row_has_tie(tie, r, S)) return;  // uniform
   const size_t rowoff = (size_t)r * C;
   const int pair_row0 = (r % R) * C;  // this row's offset within its pair
+  NV_STAMP(rm0);
   const int n = row_stage_and_build(tgt, tgt, r, C, L, tgt_mask);
+  NV_STAMP(rm1);
+  NV_STAMP_ADD0(4, rm0, rm1);  // stage + build (slots 8-12 split it)
   double *raw = (double *)(smem + L.raw);
   double *FC = (double *)(smem + L.fc);
   uint16_t *FCOL = (uint16_t *)(smem + L.fcol);
@@ -876,6 +879,13 @@ __global__ __launch_bounds__(kRowsBlock) void k_rows_match(
     nn_idx[rowoff + c] = bpos >= 0 ? pair_row0 + canon_col(TX, TY, TZ, T, n, bpos) : -1;
     nn_dist[rowoff + c] = bd;
   }
+#ifdef NAVGPU_STAMPS
+  NV_STAMP_ADD0(6, 0ull, (unsigned long long)nq);  // queries walked
+  NV_COUNT0(7);                                    // rows that built
+  __syncthreads();
+  NV_STAMP(rm2);
+  NV_STAMP_ADD0(5, rm1, rm2);  // source staging, masks and the walk (slowest lane)
+#endif
 }
 
 // K4 batches: the same fused row step with a lean LDS footprint, so that
@@ -1415,36 +1425,70 @@ __global__ __launch_bounds__(NT) void k_rows_screen32(
   const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
   const double *tg = tgt + 3 * rowoff;
   if (threadIdx.x == 0) *DT = 0u;
-  // target row features in column order (flattenPoints): positions only
+  // the offsets' origin: the row's column 0, feature or not (known before the
+  // compaction, so the row is read from HBM once)
+  const double3 o = double3{tg[0], tg[1], tg[2]};
+  // target row features in column order (flattenPoints) as f32 offsets, and
+  // Dt >= every |t - o| (inf when some offset is not a finite f32: no lane of
+  // the row is certified)
+  float dtl = 0.0f;
   const int n = compact_cols<NT>(
-      0, C, tgt_mask + rowoff, [&](int) { return 0; },
-      [&](int j, int pos, int) { FCOL[pos] = (uint16_t)j; }, RANK, scan);
+      0, C, tgt_mask + rowoff,
+      [&](int j) { return double3{tg[3 * j], tg[3 * j + 1], tg[3 * j + 2]}; },
+      [&](int j, int pos, const double3 &p) {
+        const double ex = p.x - o.x, ey = p.y - o.y, ez = p.z - o.z;
+        XF[pos] = (float)ex;
+        YF[pos] = (float)ey;
+        ZF[pos] = (float)ez;
+        FCOL[pos] = (uint16_t)j;
+        const double m = fmax(fabs(ex), fmax(fabs(ey), fabs(ez)));
+        dtl = m <= 1e37 ? fmaxf(dtl, (float)(m * (1.0 + 0x1p-20))) : INFINITY;
+        if (!(ex == ex && ey == ey && ez == ez)) dtl = INFINITY;
+      },
+      RANK, scan);
   const int nch = (n + kScreenChunk - 1) / kScreenChunk;
   const ScreenSetG G = {tg, FCOL, BOX, nch, n};
-  const double3 o = n > 0 ? G.at(0) : double3{0.0, 0.0, 0.0};
-  // f32 offsets (the last chunk's tail +inf) and Dt >= every |t - o| (inf
-  // when some offset is not a finite f32: no lane of the row is certified)
-  float dtl = 0.0f;
-  for (int e = threadIdx.x; e < nch * kScreenChunk; e += NT) {
-    float fx = INFINITY, fy = INFINITY, fz = INFINITY;
-    if (e < n) {
-      const double3 p = G.at(e);
-      const double ex = p.x - o.x, ey = p.y - o.y, ez = p.z - o.z;
-      fx = (float)ex;
-      fy = (float)ey;
-      fz = (float)ez;
-      const double m = fmax(fabs(ex), fmax(fabs(ey), fabs(ez)));
-      dtl = m <= 1e37 ? fmaxf(dtl, (float)(m * (1.0 + 0x1p-20))) : INFINITY;
-      if (!(ex == ex && ey == ey && ez == ez)) dtl = INFINITY;
-    }
-    XF[e] = fx;
-    YF[e] = fy;
-    ZF[e] = fz;
-  }
+  for (int e = n + (int)threadIdx.x; e < nch * kScreenChunk; e += NT)
+    XF[e] = YF[e] = ZF[e] = INFINITY;  // the last chunk's tail: never taken
 #pragma unroll
   for (int off = kWave / 2; off > 0; off >>= 1) dtl = fmaxf(dtl, __shfl_xor(dtl, off, kWave));
   if (lane == 0) atomicMax(DT, __float_as_uint(dtl));  // >= 0: the bits order as the values
-  screen_boxes<NT>(G, BOX, n, nch);
+  __syncthreads();  // offsets, tail and Dt
+  // chunk boxes from the f32 offsets, widened by their rounding (each offset
+  // is within 2^-24 Dt of the exact one): lower bounds on the exact f64 box
+  {
+    const double Dt0 = (double)__uint_as_float(*DT);
+    const double w = Dt0 * 0x1p-22;
+    constexpr int CPW = kWave / kScreenChunk;
+    for (int b0 = CPW * wid; b0 < nch; b0 += CPW * (NT / kWave)) {
+      const int b = b0 + lane / kScreenChunk, e = b * kScreenChunk + lane % kScreenChunk;
+      const bool in = b < nch && e < n;
+      const float v[3] = {in ? XF[e] : NAN, in ? YF[e] : NAN, in ? ZF[e] : NAN};
+      float lo[3], hi[3];
+#pragma unroll
+      for (int a = 0; a < 3; ++a) {
+        const bool ok = v[a] == v[a];
+        lo[a] = ok ? v[a] : INFINITY;
+        hi[a] = ok ? v[a] : -INFINITY;
+      }
+#pragma unroll
+      for (int off = kScreenChunk / 2; off > 0; off >>= 1)
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+          lo[a] = fminf(lo[a], __shfl_xor(lo[a], off, kWave));
+          hi[a] = fmaxf(hi[a], __shfl_xor(hi[a], off, kWave));
+        }
+      if (b < nch && lane % kScreenChunk == 0) {
+        const double oo[3] = {o.x, o.y, o.z};
+        double *bx = BOX + 6 * b;
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {  // (an all-NaN chunk keeps an empty box)
+          bx[2 * a] = (oo[a] + (double)lo[a]) - w - fabs(oo[a]) * 0x1p-50;
+          bx[2 * a + 1] = (oo[a] + (double)hi[a]) + w + fabs(oo[a]) * 0x1p-50;
+        }
+      }
+    }
+  }
   // this split's source features (compact_cols synchronises: offsets, boxes
   // and Dt are visible after it)
   const int32_t *sm = src_mask + rowoff;
@@ -1529,7 +1573,10 @@ __global__ __launch_bounds__(NT) void k_rows_screen32(
         const int k = k0 + __builtin_ctzll(m);
         m &= m - 1;
         const double lb = screen_box_lb(BOX + 6 * k, qx, qx, qy, qy, qz, qz);
-        if (__any(act && lb <= ub2())) scan32(k);
+        if (__any(act && lb <= ub2())) {
+          NV_STAMP_ADD(3, 0ull, 1ull);  // chunks scanned past the first two
+          scan32(k);
+        }
       }
     }
     // the certificate (nch = 0: no candidate, nothing to certify)
@@ -1547,6 +1594,11 @@ __global__ __launch_bounds__(NT) void k_rows_screen32(
     bool genuine = false;
     int emin = j1;
     const bool need = act && !cert;
+#ifdef NAVGPU_STAMPS
+    NV_STAMP_ADD(0, 0ull, 1ull);                                       // waves
+    NV_STAMP_ADD(1, 0ull, __any(need) ? 1ull : 0ull);                   // ... with a fallback
+    NV_STAMP_ADD(2, 0ull, (unsigned long long)__popcll(__ballot(need)));  // fallback lanes
+#endif
     if (__any(need)) {  // k_rows_screen's f64 path for these lanes
       double f1 = INFINITY, f2v = INFINITY;
       int fj = -1;

@@ -429,20 +429,23 @@ def test_split_build_query_vs_oracle(gpu, orc, monkeypatch, query_tree):
         assert (pos[r][qm[r] == 0] == -1).all()
 
 
-@pytest.mark.parametrize("seed,integer_mm", [(21, True), (5, False)])
-def test_lazy_rows_vs_oracle(gpu, orc, seed, integer_mm):
+@pytest.mark.parametrize("seed,integer_mm,R,Cc", [(5, True, 128, 2048), (5, False, 64, 1024)])
+def test_lazy_rows_vs_oracle(gpu, orc, seed, integer_mm, R, Cc):
     """kd_compact_rows_dev + kd_query_rows_lazy_dev (the shim's K5 path with
     NAVSLAM_HOST_TREES=0): a row stays in column order unless one of its
     queries met a distance tie, and then holds the reference's tree (and
     column map) exactly; every query's distance equals the oracle's KD walk
     and its position holds the coordinates of the reference's Point.
-    Integer-millimetre ranges make ties common (some rows must be rebuilt)."""
+    Integer-millimetre ranges at the K2 shape make ties common (K2i: 83 of
+    128 rows), so some rows must be rebuilt."""
     import torch
     from navslam.synth import l9_pair
-    R, Cc = 64, 1024
     lid, lid2 = l9_pair(R, Cc, seed=seed, integer_mm=integer_mm)
-    Rm = orc.rotation(1.5, -0.7, 12.0)
-    coords = np.einsum("ij,rcj->rci", Rm.reshape(3, 3), lid) + np.array([100.0, -20.0, 3.0])
+    if integer_mm:  # the K2i pair as it is: integer coordinates on both sides
+        coords = lid.copy()
+    else:           # features from one frame, coordinates from a moved one
+        Rm = orc.rotation(1.5, -0.7, 12.0)
+        coords = np.einsum("ij,rcj->rci", Rm.reshape(3, 3), lid) + np.array([100.0, -20.0, 3.0])
     dev = torch.device("cuda")
     t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
     d_lid, d_coords, d_lid2 = t(lid), t(coords), t(lid2)
