@@ -572,11 +572,16 @@ __device__ __forceinline__ uint32_t stk_enc(int flo, int fhi, int right, int d) 
 // utils/kdtree.c:110-152 over the implicit tree TX/TY/TZ[0..n): the
 // recursion's visit order (node, near subtree, then far subtree iff
 // |q[axis]-node[axis]| < best at that moment) with an explicit LIFO stack.
+//
+// stop: the query's minimum distance when the caller knows it (the screen's
+// exact minimum, for a query whose answer the tree decides only by visit
+// order), else -1. The first visited point at that distance is the answer
+// (no later point is strictly closer, kdtree.c:117), so the walk ends there.
 __device__ __forceinline__ void kd_query(const double *TX, const double *TY,
                                          const double *TZ, int n, double qx,
                                          double qy, double qz, uint32_t *stk,
                                          int stride, int *best_pos,
-                                         double *best_dist) {
+                                         double *best_dist, double stop = -1.0) {
   double best = INFINITY;
   int bpos = -1;
   int lo = 0, hi = n, depth = 0, sp = 0;
@@ -588,6 +593,10 @@ __device__ __forceinline__ void kd_query(const double *TX, const double *TY,
       if (d < best) {
         best = d;
         bpos = mid;
+        if (d == stop) {
+          sp = 0;
+          break;
+        }
       }
       const int axis = depth % 3;
       const double qa = axis == 0 ? qx : (axis == 1 ? qy : qz);
@@ -874,8 +883,9 @@ __global__ __launch_bounds__(kRowsBlock) void k_rows_match(
     const int c = QL[i];
     int bpos;
     double bd;
+    // a tied query's exact minimum came from the screen (-1: walk it all)
     kd_query(TX, TY, TZ, n, sraw[3 * c], sraw[3 * c + 1], sraw[3 * c + 2],
-             stk + threadIdx.x, blockDim.x, &bpos, &bd);
+             stk + threadIdx.x, blockDim.x, &bpos, &bd, tie ? nn_dist[rowoff + c] : -1.0);
     nn_idx[rowoff + c] = bpos >= 0 ? pair_row0 + canon_col(TX, TY, TZ, T, n, bpos) : -1;
     nn_dist[rowoff + c] = bd;
   }
@@ -1013,7 +1023,7 @@ __global__ __launch_bounds__(NT) void k_rows_match_lean(
     int bpos;
     double bd;
     kd_query(TX, TY, TZ, n, sg[3 * c], sg[3 * c + 1], sg[3 * c + 2], stk + threadIdx.x, walkers,
-             &bpos, &bd);
+             &bpos, &bd, tie ? nn_dist[rowoff + c] : -1.0);
     nn_idx[rowoff + c] = bpos >= 0 ? pair_row0 + canon_col(TX, TY, TZ, T, n, bpos) : -1;
     nn_dist[rowoff + c] = bd;
   }
@@ -1127,7 +1137,8 @@ struct ScreenSetG {
   const double *BOX;
   int nch, n;
   __device__ double3 at(int e) const {
-    const double *p = tg + 3 * (int)FCOL[min(e, max(n - 1, 0))];
+    // (clamped, and column 0 for an empty row: never a load outside the row)
+    const double *p = tg + 3 * (n > 0 ? (int)FCOL[min(max(e, 0), n - 1)] : 0);
     const double x = p[0], y = p[1], z = p[2];
     return e < n ? double3{x, y, z} : double3{INFINITY, INFINITY, INFINITY};
   }
@@ -1358,9 +1369,10 @@ __global__ __launch_bounds__(NT) void k_rows_screen(
     int emin;
     screen_verify(T, act, qx, qy, qz, d1, d2, j1, genuine, emin);
     if (act) {
-      const bool t = genuine || (d1 < INFINITY && dist > 0.0 && dist < 1e-150);
-      if (t) {
+      const bool under = d1 < INFINITY && dist > 0.0 && dist < 1e-150;
+      if (genuine || under) {
         nn_idx[rowoff + c] = kTiePending;
+        nn_dist[rowoff + c] = under ? -1.0 : dist;  // the tie pass's stop distance
         mytie = 1;
       } else {
         nn_idx[rowoff + c] = j1 >= 0 ? pair_row0 + (int)FCOL[emin] : -1;
@@ -1550,10 +1562,15 @@ __global__ __launch_bounds__(NT) void k_rows_screen32(
       scan32(s0);
       if (s1 != s0) scan32(s1);
     }
+    // the winner so far is usually the final one: its f64 point is loaded now
+    // and arrives during the box loop (gathered again below if it changed)
+    const uint32_t k1s = k1;
+    const double3 p1s = G.at((int)(k1s & idm));
+    double UB2 = ub2();  // refreshed after each further chunk scan
     const bool qok = act && qx == qx && qy == qy && qz == qz;
     double wl[3] = {qok ? qx : INFINITY, qok ? qy : INFINITY, qok ? qz : INFINITY};
     double wh[3] = {qok ? qx : -INFINITY, qok ? qy : -INFINITY, qok ? qz : -INFINITY};
-    double wd2 = qok ? ub2() : -INFINITY;
+    double wd2 = qok ? UB2 : -INFINITY;
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) {
 #pragma unroll
@@ -1573,9 +1590,10 @@ __global__ __launch_bounds__(NT) void k_rows_screen32(
         const int k = k0 + __builtin_ctzll(m);
         m &= m - 1;
         const double lb = screen_box_lb(BOX + 6 * k, qx, qx, qy, qy, qz, qz);
-        if (__any(act && lb <= ub2())) {
+        if (__any(act && lb <= UB2)) {
           NV_STAMP_ADD(3, 0ull, 1ull);  // chunks scanned past the first two
           scan32(k);
+          UB2 = ub2();
         }
       }
     }
@@ -1585,7 +1603,7 @@ __global__ __launch_bounds__(NT) void k_rows_screen32(
     bool cert = nch == 0;
     if (act && nch > 0) {
       j1 = (int)(k1 & idm);
-      const double3 p = G.at(j1);
+      const double3 p = k1 == k1s ? p1s : G.at(j1);
       const double dx = p.x - qx, dy = p.y - qy, dz = p.z - qz;
       d1 = dx * dx + dy * dy + dz * dz;  // utils/kdtree.c:16
       const float lb2 = k2 == kNoKey32 ? INFINITY : __uint_as_float(k2 & vmask);
@@ -1602,8 +1620,7 @@ __global__ __launch_bounds__(NT) void k_rows_screen32(
     if (__any(need)) {  // k_rows_screen's f64 path for these lanes
       double f1 = INFINITY, f2v = INFINITY;
       int fj = -1;
-      const double b2 = ub2();
-      screen_query(G, need, qx, qy, qz, nch > 0 ? s0 : -1, nch > 0 ? s1 : -1, f1, f2v, fj, b2);
+      screen_query(G, need, qx, qy, qz, nch > 0 ? s0 : -1, nch > 0 ? s1 : -1, f1, f2v, fj, UB2);
       bool gen;
       int em;
       screen_verify(G, need, qx, qy, qz, f1, f2v, fj, gen, em);
@@ -1616,9 +1633,10 @@ __global__ __launch_bounds__(NT) void k_rows_screen32(
     }
     if (act) {
       const double dist = __builtin_sqrt(d1);
-      const bool t = genuine || (d1 < INFINITY && dist > 0.0 && dist < 1e-150);
-      if (t) {
+      const bool under = d1 < INFINITY && dist > 0.0 && dist < 1e-150;
+      if (genuine || under) {
         nn_idx[rowoff + c] = kTiePending;
+        nn_dist[rowoff + c] = under ? -1.0 : dist;  // the tie pass's stop distance
         mytie = 1;
       } else {
         nn_idx[rowoff + c] = j1 >= 0 ? pair_row0 + (int)FCOL[emin] : -1;
@@ -1877,11 +1895,15 @@ __global__ __launch_bounds__(NT) void k_rows_query_screen(
     if (act) {
       int bpos = j1 >= 0 ? emin : -1;
       double bd = j1 >= 0 ? dist : INFINITY;
-      if (genuine || (d1 < INFINITY && dist > 0.0 && dist < 1e-150)) {
-        if (tie)  // the row holds no tree yet: k_rows_retree walks all its queries
+      const bool under = d1 < INFINITY && dist > 0.0 && dist < 1e-150;
+      if (genuine || under) {
+        if (tie) {  // the row holds no tree yet: k_rows_retree walks all its queries
           tie[r] = 1;
-        else
-          kd_query(TX, TY, TZ, n, qx, qy, qz, stk + threadIdx.x, NT, &bpos, &bd);
+          bd = under ? -1.0 : bd;  // its walk's stop distance (-1: the whole walk)
+        } else {
+          kd_query(TX, TY, TZ, n, qx, qy, qz, stk + threadIdx.x, NT, &bpos, &bd,
+                   under ? -1.0 : dist);
+        }
       }
       nn_pos[rowoff + c] = bpos;
       nn_dist[rowoff + c] = bd;
@@ -1961,7 +1983,9 @@ __global__ __launch_bounds__(kRowsBlock) void k_rows_retree(
     const double *q = queries + 3 * (rowoff + c);
     int bpos;
     double bd;
-    kd_query(TX, TY, TZ, n, q[0], q[1], q[2], stk + threadIdx.x, blockDim.x, &bpos, &bd);
+    // the screen left each query's exact minimum (-1 where it must not stop)
+    kd_query(TX, TY, TZ, n, q[0], q[1], q[2], stk + threadIdx.x, blockDim.x, &bpos, &bd,
+             nn_dist[rowoff + c]);
     if (bpos >= 0) {  // the lowest position holding bit-identical coordinates
       const long long rx = __double_as_longlong(TX[bpos]), ry = __double_as_longlong(TY[bpos]),
                       rz = __double_as_longlong(TZ[bpos]);
