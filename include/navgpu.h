@@ -243,6 +243,12 @@ void navgpu_free(navgpu_ctx *ctx, void *dptr);
  * navgpu_host_free waits for the context's streams first */
 int navgpu_host_alloc(navgpu_ctx *ctx, size_t bytes, void **hptr);
 void navgpu_host_free(navgpu_ctx *ctx, void *hptr);
+/* page-lock a caller's host range in place (copies to and from it then run by
+ * DMA, no staging). The range must stay allocated until
+ * navgpu_host_unregister; NAVGPU_ERANGE when the runtime refuses (the range
+ * stays pageable and every copy still works) */
+int navgpu_host_register(navgpu_ctx *ctx, void *hptr, size_t bytes);
+void navgpu_host_unregister(navgpu_ctx *ctx, void *hptr);
 /* stream-ordered copies on the context's stream (host memory pageable) */
 int navgpu_upload(navgpu_ctx *ctx, void *dst_dev, const void *src_host,
                   size_t bytes);

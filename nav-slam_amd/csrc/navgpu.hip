@@ -3024,6 +3024,24 @@ void navgpu_host_free(navgpu_ctx *ctx, void *hptr) {
   (void)hipHostFree(hptr);
 }
 
+int navgpu_host_register(navgpu_ctx *ctx, void *hptr, size_t bytes) {
+  ARG_CHECK(ctx && hptr && bytes);
+  const hipError_t e = hipHostRegister(hptr, bytes, hipHostRegisterDefault);
+  if (e != hipSuccess) {
+    (void)hipGetLastError();  // not sticky: the range simply stays pageable
+    set_err("hipHostRegister(%zu): %s", bytes, hipGetErrorString(e));
+    return NAVGPU_ERANGE;
+  }
+  return NAVGPU_OK;
+}
+
+void navgpu_host_unregister(navgpu_ctx *ctx, void *hptr) {
+  if (!ctx || !hptr) return;
+  (void)hipStreamSynchronize(ctx->stream);
+  if (ctx->aux) (void)hipStreamSynchronize(ctx->aux);
+  if (hipHostUnregister(hptr) != hipSuccess) (void)hipGetLastError();
+}
+
 // The per-row query over built trees (tie == nullptr), or over the
 // compacted, unbuilt rows of navgpu_kd_compact_rows_dev (tie: per-row flags,
 // then k_rows_retree on the flagged rows).

@@ -69,6 +69,8 @@ def _declare(L):
         "navgpu_free": (None, [_vp, _vp]),
         "navgpu_host_alloc": (C.c_int, [_vp, _sz, C.POINTER(_vp)]),
         "navgpu_host_free": (None, [_vp, _vp]),
+        "navgpu_host_register": (C.c_int, [_vp, _vp, _sz]),
+        "navgpu_host_unregister": (None, [_vp, _vp]),
         "navgpu_kd_rows_nodes_dev": (C.c_int, [_vp, _vp, _vp, C.c_int, C.c_int, C.c_uint64,
                                                _vp, _vp]),
         "navgpu_upload": (C.c_int, [_vp, _vp, _vp, _sz]),

@@ -55,6 +55,12 @@ int navgpu_host_alloc(navgpu_ctx *ctx, size_t bytes, void **hptr)
 }
 
 void navgpu_host_free(navgpu_ctx *ctx, void *hptr) { navgpu_free(ctx, hptr); }
+int navgpu_host_register(navgpu_ctx *ctx, void *hptr, size_t bytes)
+{
+    (void)ctx, (void)hptr, (void)bytes;
+    return 0; /* host memory is the device's here */
+}
+void navgpu_host_unregister(navgpu_ctx *ctx, void *hptr) { (void)ctx, (void)hptr; }
 
 int navgpu_upload(navgpu_ctx *ctx, void *dst_dev, const void *src_host, size_t bytes)
 {
