@@ -245,8 +245,11 @@ int navgpu_host_alloc(navgpu_ctx *ctx, size_t bytes, void **hptr);
 void navgpu_host_free(navgpu_ctx *ctx, void *hptr);
 /* page-lock a caller's host range in place (copies to and from it then run by
  * DMA, no staging). The range must stay allocated until
- * navgpu_host_unregister; NAVGPU_ERANGE when the runtime refuses (the range
- * stays pageable and every copy still works) */
+ * navgpu_host_unregister: memory freed while registered keeps the old pages
+ * behind its addresses, so a later allocation there would copy the wrong
+ * data (which is why the drop-in shim, which cannot see when its caller
+ * frees a SLAM_attr, does not use it). NAVGPU_ERANGE when the runtime
+ * refuses (the range stays pageable and every copy still works) */
 int navgpu_host_register(navgpu_ctx *ctx, void *hptr, size_t bytes);
 void navgpu_host_unregister(navgpu_ctx *ctx, void *hptr);
 /* stream-ordered copies on the context's stream (host memory pageable) */

@@ -1435,6 +1435,7 @@ __global__ __launch_bounds__(NT) void k_rows_screen32(
   int *scan = (int *)((unsigned char *)QL + align16(2 * w));
   unsigned *DT = (unsigned *)((unsigned char *)scan + align16(4 * 160));
   const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
+  NV_STAMP(z0);
   const double *tg = tgt + 3 * rowoff;
   if (threadIdx.x == 0) *DT = 0u;
   // the offsets' origin: the row's column 0, feature or not (known before the
@@ -1512,6 +1513,8 @@ __global__ __launch_bounds__(NT) void k_rows_screen32(
       nn_idx[rowoff + j] = -1;
       nn_dist[rowoff + j] = INFINITY;
     }
+  NV_STAMP(z1);
+  NV_STAMP_ADD(4, z0, z1);  // setup: compaction, offsets, boxes, query list
   const double Dt = (double)__uint_as_float(*DT);
   // key: f32 dsq bits, the low kb bits the position (nch * 32 <= 2^kb)
   const int kb = 32 - __builtin_clz((unsigned)max(nch * kScreenChunk - 1, 1));
@@ -1558,10 +1561,13 @@ __global__ __launch_bounds__(NT) void k_rows_screen32(
       const float V = __uint_as_float(k2 | idm);
       return (V < INFINITY && dl < INFINITY) ? f32_upper((double)V, dl) : (double)INFINITY;
     };
+    NV_STAMP(z2);
     if (nch > 0) {
       scan32(s0);
       if (s1 != s0) scan32(s1);
     }
+    NV_STAMP(z3);
+    NV_STAMP_ADD(5, z2, z3);  // the two start chunks
     // the winner so far is usually the final one: its f64 point is loaded now
     // and arrives during the box loop (gathered again below if it changed)
     const uint32_t k1s = k1;
@@ -1597,6 +1603,8 @@ __global__ __launch_bounds__(NT) void k_rows_screen32(
         }
       }
     }
+    NV_STAMP(z4);
+    NV_STAMP_ADD(6, z3, z4);  // the box loop and its scans
     // the certificate (nch = 0: no candidate, nothing to certify)
     int j1 = -1;
     double d1 = INFINITY;
@@ -1617,20 +1625,99 @@ __global__ __launch_bounds__(NT) void k_rows_screen32(
     NV_STAMP_ADD(1, 0ull, __any(need) ? 1ull : 0ull);                   // ... with a fallback
     NV_STAMP_ADD(2, 0ull, (unsigned long long)__popcll(__ballot(need)));  // fallback lanes
 #endif
-    if (__any(need)) {  // k_rows_screen's f64 path for these lanes
-      double f1 = INFINITY, f2v = INFINITY;
-      int fj = -1;
-      screen_query(G, need, qx, qy, qz, nch > 0 ? s0 : -1, nch > 0 ? s1 : -1, f1, f2v, fj, UB2);
-      bool gen;
-      int em;
-      screen_verify(G, need, qx, qy, qz, f1, f2v, fj, gen, em);
-      if (need) {
-        d1 = f1;
-        j1 = fj;
-        genuine = gen;
-        emin = em;
+    if (__any(need)) {
+      // Uncertified lanes. With a finite winner and finite errors the answer
+      // is decided inside the band of points whose f32 dsq could be within
+      // sqrt-equality of the minimum: f32 dsq <= f32_bound(d1 (1 + 2^-40)),
+      // d1 the winner's exact dsq (>= the true minimum). Band points (a few)
+      // get their exact dsq from the caller's row; pass 1 takes the exact
+      // minimum and runner-up over them, pass 2 (only if the runner-up has
+      // the minimum's sqrt) separates duplicates from genuine ties, as
+      // screen_verify does. The rest (non-finite data, offsets past f32
+      // range) runs k_rows_screen's f64 screen over the caller's row.
+      const bool band = need && d1 < INFINITY && Dq < 1e17 && dl < INFINITY;
+      const bool hard = need && !band;
+      if (__any(band)) {
+        const double Tb = d1 * (1.0 + 0x1p-40);
+        const float Bf = band ? f32_bound(Tb, dl) : -1.0f;
+        double e1 = INFINITY, e2 = INFINITY;
+        int ej = -1;
+        // visit(f) runs f(e, exact dsq, point) for every band point of this lane
+        auto visit = [&](auto f) {
+          for (int k = 0; k < nch; ++k) {
+            const double lb = screen_box_lb(BOX + 6 * k, qx, qx, qy, qy, qz, qz);
+            const bool in = band && lb <= Tb;
+            if (!__any(in)) continue;
+            const int e0 = k * kScreenChunk;
+            for (int u = 0; u < kScreenChunk; u += 2) {
+              const float2 xx = *(const float2 *)(XF + e0 + u);
+              const float2 yy = *(const float2 *)(YF + e0 + u);
+              const float2 zz = *(const float2 *)(ZF + e0 + u);
+              const f2 dx = f2{xx.x, xx.y} - qx2, dy = f2{yy.x, yy.y} - qy2,
+                       dz = f2{zz.x, zz.y} - qz2;
+              const f2 dd =
+                  __builtin_elementwise_fma(dz, dz, __builtin_elementwise_fma(dy, dy, dx * dx));
+#pragma unroll
+              for (int h = 0; h < 2; ++h) {
+                const bool ib = in && dd[h] <= Bf;
+                if (__any(ib) && ib) {
+                  const int e = e0 + u + h;
+                  const double3 pp = G.at(e);
+                  const double ddx = pp.x - qx, ddy = pp.y - qy, ddz = pp.z - qz;
+                  f(e, ddx * ddx + ddy * ddy + ddz * ddz, pp);  // utils/kdtree.c:16
+                }
+              }
+            }
+          }
+        };
+        visit([&](int e, double d, const double3 &) {
+          ej = d < e1 ? e : ej;
+          e2 = fmin(e2, fmax(e1, d));
+          e1 = fmin(e1, d);
+        });
+        const double edist = __builtin_sqrt(e1);
+        const bool suspect = band && ej >= 0 && __builtin_sqrt(e2) == edist;
+        bool gen = false;
+        int em = ej;
+        if (__any(suspect)) {
+          const double3 pr = G.at(ej);
+          const long long rx = __double_as_longlong(pr.x), ry = __double_as_longlong(pr.y),
+                          rz = __double_as_longlong(pr.z);
+          visit([&](int e, double d, const double3 &pp) {
+            if (suspect && __builtin_sqrt(d) == edist) {
+              const bool same = __double_as_longlong(pp.x) == rx &&
+                                __double_as_longlong(pp.y) == ry &&
+                                __double_as_longlong(pp.z) == rz;
+              gen |= !same;
+              em = same ? min(em, e) : em;
+            }
+          });
+        }
+        if (band) {
+          d1 = e1;
+          j1 = ej;
+          genuine = gen;
+          emin = em;
+        }
+      }
+      if (__any(hard)) {  // k_rows_screen's f64 path over the caller's row
+        double f1 = INFINITY, f2v = INFINITY;
+        int fj = -1;
+        screen_query(G, hard, qx, qy, qz, nch > 0 ? s0 : -1, nch > 0 ? s1 : -1, f1, f2v, fj,
+                     UB2);
+        bool gen;
+        int em;
+        screen_verify(G, hard, qx, qy, qz, f1, f2v, fj, gen, em);
+        if (hard) {
+          d1 = f1;
+          j1 = fj;
+          genuine = gen;
+          emin = em;
+        }
       }
     }
+    NV_STAMP(z5);
+    NV_STAMP_ADD(7, z4, z5);  // certificate + fallback
     if (act) {
       const double dist = __builtin_sqrt(d1);
       const bool under = d1 < INFINITY && dist > 0.0 && dist < 1e-150;

@@ -331,7 +331,6 @@ typedef struct {
     void *d_nodes;          /* KDNode image of the row trees, device */
     KDNode *h_nodes;        /* its host copy: the trees handed out */
     int h_nodes_pinned;
-    void *map_pinned; /* attr->globalPointCloud, page-locked in place (or NULL) */
     int32_t h_off[ROWS + 1];
     NeighborResult *result; /* correspondence list (src/slam.c:214) */
 } slam_state;
@@ -455,26 +454,9 @@ static void map_frame(SLAM_attr *attr, slam_state *s, Pos pos,
     PROF_ADD(1, pt1);
 }
 
-/* The map slots are written by the device every frame (src/slam.c:395): the
- * SLAM_attr array is page-locked in place so the slot comes back by DMA
- * instead of through the runtime's staging buffer. Done at every init_slam:
- * a SLAM_attr at a recycled address gets its own pages locked. Refused (a
- * lock limit, say): the copies stay pageable. */
-static void pin_map(SLAM_attr *attr, slam_state *s)
-{
-    navgpu_ctx *c = ctx();
-    if (s->map_pinned)
-        navgpu_host_unregister(c, s->map_pinned);
-    s->map_pinned = NULL;
-    void *p = &attr->globalPointCloud[0];
-    if (navgpu_host_register(c, p, sizeof(attr->globalPointCloud)) == NAVGPU_OK)
-        s->map_pinned = p;
-}
-
 void init_slam(SLAM_attr *attr, Pos pos, PointCloud *lidarPointCloud)
 {
     slam_state *s = state_for(attr);
-    pin_map(attr, s);
     attr->frameCount = 0;
     attr->error = 0.0;
     map_frame(attr, s, pos, lidarPointCloud, 0);

@@ -36,6 +36,7 @@ ms, n = g.timing_read("rows_match")
 have = g.L.navgpu_debug_stamps(st) == 0
 out = {"lib": os.path.basename(a.lib or "libnavgpu.so"), "rows_match_us": 1000 * ms / max(n, 1)}
 if have:
+    out["slots"] = [int(x) for x in st]
     out.update({"screen_waves": int(st[0]), "fallback_waves": int(st[1]),
                 "fallback_lanes": int(st[2]), "extra_chunks_per_wave": round(st[3] / max(st[0], 1), 2)})
     nb = max(int(st[7]), 1)
