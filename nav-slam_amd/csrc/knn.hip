@@ -1211,6 +1211,11 @@ constexpr int kWPairs = kWRec / 2 + 2;   // two spare pairs: read-ahead
 constexpr int kWZg = 4 * kWPairs;        // floats from the XY plane to the ZG plane
 constexpr int kWCols = 2 * kWave;        // staged columns per round: two per lane
 constexpr int kWSegs = 8;                // segments (grid rows) per round
+// waves per workgroup, each with its own chunk and LDS region
+#ifndef NAVGPU_KNNW_WPB
+#define NAVGPU_KNNW_WPB 1
+#endif
+constexpr int kWPB = NAVGPU_KNNW_WPB;
 #ifndef NAVGPU_KNNW_U
 #define NAVGPU_KNNW_U 1
 #endif
@@ -1251,7 +1256,7 @@ __device__ __forceinline__ WFrame wframe(const GridParams &G, int xf, int xl, in
 constexpr int kWStampChunks = 1 << 15;
 __device__ unsigned long long g_wstamps[kWStampChunks][8];
 #define NV_WFLUSH(chunk)                                             \
-  if (threadIdx.x == 0 && (chunk) < kWStampChunks) {                 \
+  if ((threadIdx.x & 63) == 0 && (chunk) < kWStampChunks) {          \
     _Pragma("unroll") for (int s_ = 1; s_ < 9; ++s_)                 \
       g_wstamps[chunk][s_ - 1] = nv_acc[s_];                         \
   }
@@ -1260,28 +1265,35 @@ __device__ unsigned long long g_wstamps[kWStampChunks][8];
 #endif
 
 template <int K>
-__global__ __launch_bounds__(kWave, NAVGPU_KNNW_MINW) void k_knnw(const GridParams *__restrict__ gp,
+__global__ __launch_bounds__(kWave * kWPB, NAVGPU_KNNW_MINW) void k_knnw(const GridParams *__restrict__ gp,
                                                    const int *__restrict__ tstart,
                                                    const PRec *__restrict__ tsort,
                                                    const SRec *__restrict__ srec,
                                                    const QSide QS, int nq, int ntg,
                                                    int32_t *__restrict__ oidx,
                                                    double *__restrict__ odist, KnnLists L_) {
-  __shared__ __attribute__((aligned(16))) float spair[2 * kWZg];
-  __shared__ int colst[kWCols + 1];  // first slot of virtual column v; [kWCols] = total
+  // one region per wave of the workgroup (the waves never synchronise)
+  __shared__ __attribute__((aligned(16))) float spair_w[kWPB][2 * kWZg];
+  __shared__ int colst_w[kWPB][kWCols + 1];  // first slot of virtual column v; [kWCols] = total
   // each segment's 9 row pieces: [sbnd[s][r][0], sbnd[s][r][1])
-  __shared__ int sbnd[kWSegs][9][2];
+  __shared__ int sbnd_w[kWPB][kWSegs][9][2];
+  const int wid = kWPB > 1 ? (int)threadIdx.x / kWave : 0;
+  float *spair = spair_w[wid];
+  int *colst = colst_w[wid];
+  int(*sbnd)[9][2] = sbnd_w[wid];
   constexpr int KL = K + 1;
   static_assert(K >= 1 && K <= 16, "K");
   const GridParams G = *gp;
   const int S = G.sx;
   const int g0 = G.g[0], g1 = G.g[1], g2 = G.g[2];
-  // chunks dealt to the 8 XCDs in contiguous ranges (block b -> XCD b % 8)
+  // chunks dealt to the 8 XCDs in contiguous ranges (block b -> XCD b % 8),
+  // kWPB consecutive chunks per workgroup
   const int nchunk = (nq + kWave - 1) / kWave;
   const int per = (nchunk + 7) / 8;
-  const int chunk = (int)(blockIdx.x & 7) * per + (int)(blockIdx.x >> 3);
-  if (chunk >= nchunk) return;
-  const int lane = (int)threadIdx.x;
+  const int cx = (int)(blockIdx.x >> 3) * kWPB + wid;
+  const int chunk = (int)(blockIdx.x & 7) * per + cx;
+  if (cx >= per || chunk >= nchunk) return;  // (no workgroup barrier follows)
+  const int lane = (int)threadIdx.x & (kWave - 1);
   NV_ACC_DECL;
   NV_STAMP(w0);
   const int nlive = min(kWave, nq - chunk * kWave);
@@ -2163,7 +2175,7 @@ static int knn_run(navgpu_ctx *ctx, const double *tgt, size_t nt, const double *
   // k_knnw: one 64-lane block per chunk of 64 cell-sorted queries, chunks
   // dealt to the XCDs in contiguous ranges
   const int nchunk = (int)((nq + kWave - 1) / kWave);
-  const dim3 gw(8 * ((nchunk + 7) / 8)), bw(kWave);
+  const dim3 gw(8 * (((nchunk + 7) / 8 + kWPB - 1) / kWPB)), bw(kWave * kWPB);
   const bool waves = ctx->knn_mode == 1;
   const QSide QS{queries, qperm, qcell};
 #define KNN_CASE(KK)                                                                        \

@@ -19,3 +19,4 @@ for r in 1 2; do
   b k2_f32 "NAVGPU_SCREEN_F32=1" "--workload k2" || exit 1
   b k2_f64 "NAVGPU_SCREEN_F32=0" "--workload k2" || exit 1
 done
+echo "== k_knnw waves per workgroup"; VDIR=nav-slam_amd/lib/variants bash scripts/r4_var.sh "$TAG/vw" 2 || exit $?
