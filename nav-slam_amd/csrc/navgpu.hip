@@ -149,6 +149,64 @@ __device__ __forceinline__ int tape_jump(int p, int sp, unsigned long long lbelo
   return p - k * q;
 }
 
+// The same nth_element for a window of at most 64 positions, held in the
+// wave's registers (lane l = position first + l) from its first pass to its
+// last (r4): a pass is two ballots, the tape chains resolved by shuffles, two
+// forward permutes (ds_permute) and one key read; P is written once at the
+// end. The window shrinks in lane space ([a, b]); lanes outside keep their
+// final elements.
+#ifndef NAVGPU_WAVE_REGS
+#define NAVGPU_WAVE_REGS 1
+#endif
+constexpr bool kWaveRegs = NAVGPU_WAVE_REGS;
+template <class IdxT>
+__device__ void wave_nth_element_regs(const double *key, IdxT *P, int first, int last,
+                                      int nth, int lane) {
+  const int len = last - first + 1;  // <= 64
+  int e = lane < len ? (int)P[first + lane] : 0;
+  double k = key[e];
+  const unsigned long long below = (1ull << lane) - 1ull;
+  const int nl = nth - first;
+  int a = 0, b = len - 1;
+  while (a < b) {
+    const int pe = __shfl(e, b, kWave);
+    const double pk = __shfl(k, b, kWave);
+    const bool inw = lane >= a && lane < b;
+    const bool small = inw && ((k - pk) <= 0.0);  // kdtree.c:31-43
+    const unsigned long long bal = __ballot(small);
+    const unsigned long long lbal = __ballot(inw && !small);
+    const int sp = a + __popcll(bal & below);  // a small's destination lane
+    const int ps = a + __popcll(bal);          // the pivot's lane
+    // tape word: bit 31 = resolved element, else the lane it equals
+    unsigned w = 0x80000000u | (unsigned)e;
+    if (small && sp != lane) w = (unsigned)tape_jump(lane, sp, lbal & below, 0);
+    while (__ballot(!(w >> 31))) {
+      const unsigned o = __shfl(w, (w >> 31) ? lane : (int)(w & (kWave - 1)), kWave);
+      if (!(w >> 31)) w = o;
+    }
+    const int tv = (int)(w & 0x7fffffffu);
+    // smalls to a .. ps-1; tape[ps] to b, tape[ps+1 .. b-1] stay; pivot at ps
+    // (lanes with nothing to send write the pivot's lane, which takes pe)
+    const int v1 = __builtin_amdgcn_ds_permute((small ? sp : ps) * 4, e);
+    const bool tl = lane >= ps && lane < b;
+    const int v2 = __builtin_amdgcn_ds_permute((tl ? (lane == ps ? b : lane) : ps) * 4, tv);
+    if (lane >= a && lane < ps)
+      e = v1;
+    else if (lane == ps)
+      e = pe;
+    else if (lane > ps && lane <= b)
+      e = v2;
+    k = key[e];
+    if (ps == nl) break;
+    if (ps < nl)
+      a = ps + 1;
+    else
+      b = ps - 1;
+  }
+  if (lane < len) P[first + lane] = (IdxT)e;
+  wave_sync_mem();  // the writes before the next pass reads P
+}
+
 template <class IdxT, bool GMEM = false>
 __device__ void wave_nth_element(const double *key, IdxT *P, IdxT *T,
                                  int first, int last, int nth, int lane) {
@@ -158,6 +216,10 @@ __device__ void wave_nth_element(const double *key, IdxT *P, IdxT *T,
   // chunk's P/key reads are issued before the current chunk resolves (this
   // chunk only writes positions below the next chunk).
   while (first < last) {
+    if (!GMEM && kWaveRegs && last - first < kWave) {
+      wave_nth_element_regs(key, P, first, last, nth, lane);
+      return;
+    }
     const int pe = (int)P[last];
     const double pk = key[pe];
     const int m = last - first;
