@@ -1126,9 +1126,19 @@ __host__ __device__ inline int rows_screen_lds(int C, int w) {
 // ranked. Writes put(j, rank, load(j)) for each kept column and, when rank_at != null,
 // rank_at[j] = the number of kept columns before j (every j in [c0, c1)).
 // cnt: LDS, >= U * NT / 64 + 1 ints. Returns the count; synchronises.
+template <int NT, class Flag, class Load, class Put>
+__device__ int compact_cols_f(int c0, int c1, Flag flag, Load load, Put put, uint16_t *rank_at,
+                              int *cnt);
 template <int NT, class Load, class Put>
 __device__ int compact_cols(int c0, int c1, const int32_t *__restrict__ mask, Load load,
                             Put put, uint16_t *rank_at, int *cnt) {
+  return compact_cols_f<NT>(
+      c0, c1, [&](int j) { return mask[j] != 0; }, load, put, rank_at, cnt);
+}
+// the same with the keep test a functor (called once per column in [c0, c1))
+template <int NT, class Flag, class Load, class Put>
+__device__ int compact_cols_f(int c0, int c1, Flag flag, Load load, Put put, uint16_t *rank_at,
+                              int *cnt) {
   using Val = decltype(load(0));
   constexpr int NW = NT / kWave, U = 4;
   const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
@@ -1140,12 +1150,15 @@ __device__ int compact_cols(int c0, int c1, const int32_t *__restrict__ mask, Lo
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int j = j0 + u * NT + (int)threadIdx.x;
-      f[u] = j < c1 && mask[j] != 0;
+      // (evaluated at a clamped column, unconditionally: a condition around
+      // a load makes hipcc branch and wait per element; a flag with side
+      // effects must tolerate a repeated column)
+      f[u] = (j < c1) & (bool)flag(min(j, c1 - 1));
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {  // the kept columns' loads, all in flight
       const int j = j0 + u * NT + (int)threadIdx.x;
-      if (f[u]) v[u] = load(j);
+      v[u] = load(min(j, c1 - 1));  // (unconditional, as the flags)
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -1479,8 +1492,9 @@ __host__ __device__ inline int rows_screen32_lds(int C, int w) {
 template <int NT>
 __global__ __launch_bounds__(NT) void k_rows_screen32(
     const double *__restrict__ src, const double *__restrict__ tgt, int R, int C,
-    const int32_t *__restrict__ src_mask, const int32_t *__restrict__ tgt_mask,
-    int32_t *__restrict__ nn_idx, double *__restrict__ nn_dist, int32_t *__restrict__ tie) {
+    int32_t *__restrict__ src_mask, int32_t *__restrict__ tgt_mask,
+    int32_t *__restrict__ nn_idx, double *__restrict__ nn_dist, int32_t *__restrict__ tie,
+    int fuse) {
   const int r = blockIdx.x, S = gridDim.y, sp = blockIdx.y;
   const int w = (C + S - 1) / S;
   const int c0 = sp * w, c1 = min(C, c0 + w);
@@ -1507,8 +1521,17 @@ __global__ __launch_bounds__(NT) void k_rows_screen32(
   // Dt >= every |t - o| (inf when some offset is not a finite f32: no lane of
   // the row is certified)
   float dtl = 0.0f;
-  const int n = compact_cols<NT>(
-      0, C, tgt_mask + rowoff,
+  // features: from the masks k_curvature wrote, or (fuse) the curvature
+  // itself from the rows (src/slam.c:16-58; split 0 writes the target mask
+  // when the caller wants it)
+  const int n = compact_cols_f<NT>(
+      0, C,
+      [&](int j) -> int {
+        if (!fuse) return tgt_mask[rowoff + j] != 0;
+        const int f = row_feature_global(tg, C, j);
+        if (tgt_mask && sp == 0) tgt_mask[rowoff + j] = f;
+        return f;
+      },
       [&](int j) { return double3{tg[3 * j], tg[3 * j + 1], tg[3 * j + 2]}; },
       [&](int j, int pos, const double3 &p) {
         const double ex = p.x - o.x, ey = p.y - o.y, ez = p.z - o.z;
@@ -1566,15 +1589,25 @@ __global__ __launch_bounds__(NT) void k_rows_screen32(
   }
   // this split's source features (compact_cols synchronises: offsets, boxes
   // and Dt are visible after it)
-  const int32_t *sm = src_mask + rowoff;
-  const int nq = compact_cols<NT>(
-      c0, c1, sm, [&](int) { return 0; }, [&](int j, int pos, int) { QL[pos] = (uint16_t)j; },
-      nullptr, scan);
-  for (int j = c0 + (int)threadIdx.x; j < c1; j += NT)
-    if (!sm[j]) {
-      nn_idx[rowoff + j] = -1;
-      nn_dist[rowoff + j] = INFINITY;
-    }
+  const double *sg = src + 3 * rowoff;
+  const int nq = compact_cols_f<NT>(
+      c0, c1,
+      [&](int j) -> int {
+        int f;
+        if (fuse) {
+          f = row_feature_global(sg, C, j);
+          if (src_mask) src_mask[rowoff + j] = f;
+        } else {
+          f = src_mask[rowoff + j] != 0;
+        }
+        if (!f) {  // no feature, no correspondence
+          nn_idx[rowoff + j] = -1;
+          nn_dist[rowoff + j] = INFINITY;
+        }
+        return f;
+      },
+      [&](int) { return 0; }, [&](int j, int pos, int) { QL[pos] = (uint16_t)j; }, nullptr,
+      scan);
   NV_STAMP(z1);
   NV_STAMP_ADD(4, z0, z1);  // setup: compaction, offsets, boxes, query list
   const double Dt = (double)__uint_as_float(*DT);
@@ -3367,14 +3400,25 @@ int rows_match_launch(navgpu_ctx *ctx, const double *src, const double *tgt, int
   TimedRegion tr(ctx, "rows_match");
   if (screen) {
     const size_t N = (size_t)rows * C;
-    if (!src_mask) RC(ws(ctx, kRowMaskS, N, &src_mask));
-    if (!tgt_mask) RC(ws(ctx, kRowMaskT, N, &tgt_mask));
+    const char *f32e = getenv("NAVGPU_SCREEN_F32");
+    const bool f32 = !(f32e && *f32e == '0');
+    // the f32 screen computes the features itself (no k_curvature pass, no
+    // mask round trip through HBM); the masks are written only if asked for
     // column splits: >= 512 workgroups in all (two per CU: ~64 KB of LDS
     // each), >= 128 columns each; 512 threads once a split holds >= 512
     // columns (measured: K2 83 us at S = 4 x 512 threads, 102 us at S = 8 x
     // 256; a K4 batch is fastest unsplit at 512 threads)
     while (S < 8 && (long long)rows * S < 512 && C / (2 * S) >= 128) S <<= 1;
     if (const char *e = getenv("NAVGPU_SCREEN_S")) S = std::max(1, std::min(64, atoi(e)));
+    // unsplit rows (batches): the f32 screen computes the features itself
+    // (r4: K4 5.43 -> 5.04 ms; split rows would each redo the target row's:
+    // K2 79 -> 84 us, so they keep k_curvature)
+    const char *fue = getenv("NAVGPU_SCREEN_FUSE");
+    const bool fuse = f32 && (fue ? *fue != '0' : S == 1);
+    if (!fuse) {
+      if (!src_mask) RC(ws(ctx, kRowMaskS, N, &src_mask));
+      if (!tgt_mask) RC(ws(ctx, kRowMaskT, N, &tgt_mask));
+    }
     const int w = (C + S - 1) / S;
     int32_t *tf;
     RC(ws(ctx, kRowTie, (size_t)rows * S, &tf));
@@ -3382,7 +3426,7 @@ int rows_match_launch(navgpu_ctx *ctx, const double *src, const double *tgt, int
     ctx->screen_rows = rows;
     ctx->screen_S = S;
     // R1 on both clouds, <= 65535 rows per launch (grid y)
-    for (int r0 = 0; r0 < rows; r0 += 65535) {
+    for (int r0 = 0; r0 < rows && !fuse; r0 += 65535) {
       const int nr = std::min(rows - r0, 65535);
       const size_t o = (size_t)r0 * C;
       CurvJob J = {{src + 3 * o, tgt + 3 * o}, {src_mask + o, tgt_mask + o}, {nullptr, nullptr}};
@@ -3390,22 +3434,22 @@ int rows_match_launch(navgpu_ctx *ctx, const double *src, const double *tgt, int
                          dim3(kCurvTile), 0, ctx->stream, J, nr, C);
       CHECK_LAUNCH("k_curvature");
     }
-    const char *f32e = getenv("NAVGPU_SCREEN_F32");
-    const bool f32 = !(f32e && *f32e == '0');
     const int lds = f32 ? rows_screen32_lds(C, w) : rows_screen_lds(C, w);
     if (lds > lds_limit()) {
       set_err("rows_screen: C=%d needs %d B of LDS (device limit %d)", C, lds, lds_limit());
       return NAVGPU_ERANGE;
     }
     const char *nte = getenv("NAVGPU_SCREEN_NT");
-    if (f32 && (nte ? atoi(nte) == 512 : w >= 512)) {
+    // f32 screen: 256-thread workgroups for unsplit rows (r4: K4 5.04 ->
+    // 4.12 ms: twice the resident rows per CU at the same waves)
+    if (f32 && (nte ? atoi(nte) == 512 : (w >= 512 && S > 1))) {
       RC(set_lds(k_rows_screen32<512>, lds));
       hipLaunchKernelGGL(k_rows_screen32<512>, dim3(rows, S), dim3(512), lds, ctx->stream, src,
-                         tgt, R, C, src_mask, tgt_mask, nn_idx, nn_dist, tf);
+                         tgt, R, C, src_mask, tgt_mask, nn_idx, nn_dist, tf, (int)fuse);
     } else if (f32) {
       RC(set_lds(k_rows_screen32<256>, lds));
       hipLaunchKernelGGL(k_rows_screen32<256>, dim3(rows, S), dim3(256), lds, ctx->stream, src,
-                         tgt, R, C, src_mask, tgt_mask, nn_idx, nn_dist, tf);
+                         tgt, R, C, src_mask, tgt_mask, nn_idx, nn_dist, tf, (int)fuse);
     } else if (nte ? atoi(nte) == 512 : w >= 512) {
       RC(set_lds(k_rows_screen<512>, lds));
       hipLaunchKernelGGL(k_rows_screen<512>, dim3(rows, S), dim3(512), lds, ctx->stream, src,

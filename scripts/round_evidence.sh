@@ -5,7 +5,11 @@
 #   --pmc runs, no trace domains) -> traffic_<w>.json -> the bench lines, each
 #   quoting its own traffic json (K3 also with the CPU baseline).
 # A crash/abort/timeout ends the script. SKIP_TESTS=1 skips pytest + smoke.
+# PARTS (default "tests k3 pmc bench") picks the sections, so the session can
+# be split over several gpurun calls.
 TAG=${1:-r3}
+PARTS=${PARTS:-tests k3 pmc bench}
+part() { case " $PARTS " in *" $1 "*) return 0;; esac; return 1; }
 OUT=gpurun_out/$TAG
 mkdir -p "$OUT"
 export NAVSLAM_QUIET=1 PYTHONUNBUFFERED=1
@@ -20,17 +24,19 @@ step() {  # step <name> <timeout> cmd...
   if fatal $rc; then echo "FATAL in $name, stopping"; exit $rc; fi
   return 0
 }
-if [ -z "$SKIP_TESTS" ]; then
+if [ -z "$SKIP_TESTS" ] && part tests; then
   step pytest 900 python3 -u -m pytest tests -m gpu -v -x --timeout 240 --timeout-method=thread
   step smoke 300 python3 -c "import __graft_entry__ as g; g.smoke()"
 fi
 export TMPDIR=/tmp
 Q="--no-cpu-baseline --no-traffic-json --no-stream-copy"
+if part k3; then
 step trace_k3 600 rocprofv3 --kernel-trace --stats -d "$OUT/trace_k3" -o run --output-format csv -- python3 bench.py --steps 20 --warmup 3 $Q --json-out "$OUT/bench_k3_traced.json"
 # one pair at a time: the trace's per-launch kernel sums and the line's HIP
 # events time the same isolated kernels
 step trace_k3_iso 600 rocprofv3 --kernel-trace --stats -d "$OUT/trace_k3_iso" -o run --output-format csv -- python3 bench.py --inflight 1 --steps 20 --warmup 3 $Q --json-out "$OUT/bench_k3_iso_traced.json"
 step trace_check 60 python3 scripts/trace_check.py "$(find "$OUT/trace_k3_iso" -name "*kernel_stats.csv" | head -1)" "$OUT/bench_k3_iso_traced.json" "$OUT/trace_check_k3.json"
+fi
 pmc() {  # pmc <w> <traffic args> -- <bench args>
   local w=$1; shift
   local targs=()
@@ -42,12 +48,15 @@ pmc() {  # pmc <w> <traffic args> -- <bench args>
   W=$(find "$OUT/pmc_write_$w" -name "*counter_collection.csv" | head -1)
   step traffic_$w 120 python3 scripts/traffic_json.py "$F" "$W" "$OUT/traffic_$w.json" "$TAG" --workload "$w" "${targs[@]}" --src "python3 bench.py $*"
 }
-pmc k3 -- --steps 20 --warmup 3
+if part k3; then pmc k3 -- --steps 20 --warmup 3; fi
+if part pmc; then
 pmc k2 --points 262144 --pairs 1 -- --workload k2 --steps 10
 pmc k2i --points 262144 --pairs 1 -- --workload k2 --integer-mm --steps 10
 pmc k4 --points 262144 --pairs 256 -- --workload k4 --steps 2 --warmup 1
 pmc k4i --points 262144 --pairs 256 -- --workload k4 --integer-mm --steps 2 --warmup 1
 pmc k5f --points 262144 -- --workload k5 --k5-mode fast --steps 20 --warmup 2
+fi
+if part bench; then
 step bench_k3 600 python3 bench.py --traffic-json "$OUT/traffic_k3.json" --json-out "$OUT/bench_k3.json"
 step bench_k3_inflight1 300 python3 bench.py --inflight 1 --no-cpu-baseline --traffic-json "$OUT/traffic_k3.json" --json-out "$OUT/bench_k3_inflight1.json"
 step bench_k2 300 python3 bench.py --workload k2 --steps 10 --traffic-json "$OUT/traffic_k2.json" --json-out "$OUT/bench_k2.json"
@@ -56,5 +65,7 @@ step bench_k4 400 python3 bench.py --workload k4 --steps 3 --warmup 1 --traffic-
 step bench_k4i 400 python3 bench.py --workload k4 --integer-mm --steps 3 --warmup 1 --traffic-json "$OUT/traffic_k4i.json" --json-out "$OUT/bench_k4i.json"
 step bench_k5 400 python3 bench.py --workload k5 --steps 30 --warmup 2 --json-out "$OUT/bench_k5.json"
 step bench_k5_fast 400 python3 bench.py --workload k5 --k5-mode fast --steps 30 --warmup 2 --traffic-json "$OUT/traffic_k5f.json" --json-out "$OUT/bench_k5_fast.json"
+NAVSLAM_HOST_TREES=0 step bench_k5_fast_lazy 400 python3 bench.py --workload k5 --k5-mode fast --steps 30 --warmup 2 --no-traffic-json --json-out "$OUT/bench_k5_fast_lazy.json"
 step trace_k5 400 rocprofv3 --kernel-trace --stats -d "$OUT/trace_k5" -o run --output-format csv -- python3 bench.py --workload k5 --k5-mode fast --steps 20 --warmup 2 --no-cpu-baseline --no-traffic-json
+fi
 echo done
