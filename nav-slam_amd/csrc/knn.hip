@@ -1204,7 +1204,7 @@ __global__ __launch_bounds__(kTileThreads, kKnnMinWaves) void k_knn(
 #define NAVGPU_KNNW_REC 800
 #endif
 #ifndef NAVGPU_KNNW_MINW
-#define NAVGPU_KNNW_MINW 3
+#define NAVGPU_KNNW_MINW 4  // (r4 A/B: query 165 -> 161 us against 3)
 #endif
 constexpr int kWRec = NAVGPU_KNNW_REC;   // staged records per wave (16 B each)
 constexpr int kWPairs = kWRec / 2 + 2;   // two spare pairs: read-ahead

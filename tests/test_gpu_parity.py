@@ -548,7 +548,7 @@ def test_knn_hard_cases(gpu, orc, k):
 
 @pytest.mark.parametrize("sx", [1, 2, 3, 8])
 def test_knn_cell_slicing_variants(orc, sx, monkeypatch):
-    """NAVGPU_KNN_SX (x cells per h; default 4) reshapes every tile, block
+    """NAVGPU_KNN_SX (x cells per h; default 3) reshapes every tile, block
     and certificate reach: each setting gives the brute-force answer, on
     uniform, integer-mm and clustered data, k = 2, 8 and 13."""
     from navslam.gpu import NavGpu
