@@ -536,6 +536,10 @@ __global__ __launch_bounds__(256) void k_bin_scatter(BinJob J, const GridParams 
 // first kBinFineHold * blockDim points stay in registers between the count
 // and the placement and the rest are re-read.
 constexpr int kFineStage = 2048;
+#ifndef NAVGPU_FINE_TSTAGE
+#define NAVGPU_FINE_TSTAGE 1
+#endif
+constexpr bool kFineTStage = NAVGPU_FINE_TSTAGE;
 constexpr int kFineStageHold = kFineStage / kBinFineThreads;
 // dynamic LDS: cnt[2^shift], then lslot[kFineStage] when queries are staged
 constexpr size_t fine_lds_bytes(int shift, bool stage_q) {
@@ -555,7 +559,10 @@ __global__ __launch_bounds__(kBinFineThreads) void k_bin_fine(BinJob J,
   const int ncell = 1 << J.shift, base = b << J.shift;
   const int lo = bbase[side * (J.nb + 1) + b], hi = bbase[side * (J.nb + 1) + b + 1];
   const int n = hi - lo;
-  const bool staged = side && n <= qstage;
+  // staged placement: the queries' (qstage > 0) and, since r4, the targets'
+  // (NAVGPU_FINE_TSTAGE): output positions are written in order, coalesced;
+  // the scattered 32-B PRec / 16-B SRec stores cost partial-line writes
+  const bool staged = n <= qstage && (side || kFineTStage);
   const BinPt *src = S.bin;
   const QKey *qk = S.key;
   const int bd = (int)blockDim.x, tid = (int)threadIdx.x;
@@ -569,7 +576,7 @@ __global__ __launch_bounds__(kBinFineThreads) void k_bin_fine(BinJob J,
 #pragma unroll
     for (int u = 0; u < kFineStageHold; ++u) {
       const int sl = u * bd + tid;
-      if (sl < n) scell[u] = qk[lo + sl].cell;
+      if (sl < n) scell[u] = side ? qk[lo + sl].cell : src[lo + sl].cell;
     }
 #pragma unroll
     for (int u = 0; u < kFineStageHold; ++u)
@@ -620,10 +627,31 @@ __global__ __launch_bounds__(kBinFineThreads) void k_bin_fine(BinJob J,
       if (sl < n) lslot[atomicAdd(&cnt[scell[u] - base], 1) - lo] = (uint16_t)sl;
     }
     __syncthreads();
-    for (int j = tid; j < n; j += bd) {
-      const QKey e = qk[lo + lslot[j]];
-      S.perm[lo + j] = e.idx;
-      S.qcell[lo + j] = e.cell;
+    if (side) {
+      for (int j = tid; j < n; j += bd) {
+        const QKey e = qk[lo + lslot[j]];
+        S.perm[lo + j] = e.idx;
+        S.qcell[lo + j] = e.cell;
+      }
+    } else {
+      for (int j = tid; j < n; j += bd) {
+        const BinPt e = src[lo + lslot[j]];  // (the bucket's records are in L2)
+        PRec t;
+        t.x = e.x;
+        t.y = e.y;
+        t.z = e.z;
+        t.idx = e.idx;
+        const int row = e.cell / g0;
+        t.cx = e.cell - row * g0;
+        S.sorted[lo + j] = t;
+        const int cy = row % g1, cz = row / g1;
+        SRec r;
+        r.x = (float)(e.x - (G.o[0] + (t.cx + 0.5) * G.e[0]));
+        r.y = (float)(e.y - (G.o[1] + (cy + 0.5) * G.e[1]));
+        r.z = (float)(e.z - (G.o[2] + (cz + 0.5) * G.e[2]));
+        r.cx = t.cx;
+        S.srec[lo + j] = r;
+      }
     }
     return;
   }
