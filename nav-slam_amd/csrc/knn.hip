@@ -10,21 +10,27 @@
 //
 // Pipeline of one call (DESIGN.md §3-§4 has the HBM layout and the roofline
 // of each kernel):
-//   k_bbox_partial, k_bin_hist      target bbox -> uniform grid (cells of
-//                                   h/sx x h x h, ~occ targets per h^3)
+//   k_bbox_partial                  target bbox partials
 //   k_bin_hist, k_bin_colscan, k_bin_scatter, k_bin_fine
-//                                   both clouds counting-sorted by cell
-//                                   (LDS atomics only): the targets as
-//                                   cell-sorted 32-B records (f64 point,
-//                                   index, x column), the queries as a
-//                                   cell-sorted permutation (4 B) of their
-//                                   coarse-bucketed records
-//   k_knn<K>                        tiles of one grid row: the 9 neighbouring
-//                                   row segments staged in LDS (column-major),
-//                                   one query per lane: packed-f32 screen,
-//                                   survivors filtered into an LDS list and a
-//                                   sorted top-(K+1), f64 exact stage, a
-//                                   certificate that the answer is exact
+//                                   both clouds counting-sorted by cell of a
+//                                   uniform grid (cells h/sx x h x h, ~occ
+//                                   targets per h^3; every k_bin_hist block
+//                                   derives the grid from the partials) with
+//                                   LDS atomics only: the targets as
+//                                   cell-sorted 32-B PRec records (f64 point,
+//                                   index, x column) and 16-B SRec staging
+//                                   records (f32 offset from the cell centre),
+//                                   the queries as a cell-sorted permutation
+//                                   and their cells
+//   k_knnw<K>                       (default) one wave per chunk of 64
+//                                   cell-sorted queries: the chunk's row
+//                                   pieces staged in LDS column-major, one
+//                                   query per lane: packed-f32 keys into a
+//                                   sorted top-(K+1) (v_med3 insertion), f64
+//                                   exact stage, a certificate that the
+//                                   answer is exact
+//   k_knn<K>                        (NAVGPU_KNN_MODE=0) the r3 tile form of
+//                                   the same pass, kept for A/B
 //   k_knn_slow<K>                   the uncertified rest, one wave per query
 #include "navgpu_common.h"
 
@@ -786,19 +792,20 @@ __device__ __forceinline__ void push_slow(const KnnLists &L_, int qi, double thr
 // One query per lane (cell-sorted queries, read coalesced). The block is
 // walked in pairs of records from its even-aligned first slot ta: packed f32
 // squared distances (3 packed sub, 1 mul, 2 fma per pair), keys packed with
-// the wave-uniform pair offset as local id. A key enters the lane's LDS list
-// only if it is below the lane's threshold T: at first the f32 image of R^2,
-// R the radius holding ~lambda targets at the block's density; after each
-// drain, the (K+1)-th key of the lane's sorted list. A drain (when some lane's
-// list is nearly full, and at the end) inserts the listed keys into the sorted
-// K+1 smallest by a branch-free median-of-3 network. So the network runs on
-// the ~lambda survivors, not on all ~100 candidates of the block.
+// the wave-uniform pair offset as local id. By default every key goes
+// straight into the lane's sorted K+1 smallest (a branch-free median-of-3
+// network). With NAVGPU_KNN_LIST=1 (off: its LDS costs a resident block per
+// CU) a key is first appended to a per-lane LDS list if it is below the
+// lane's threshold T (at first the f32 image of R^2, R the radius holding
+// ~lambda targets at the block's density; after each drain, the (K+1)-th
+// key), and drains insert the listed keys in batches.
 //
 // Exact stage and certificate. The K best keys are re-evaluated with the
 // reference f64 formula from the cell-sorted f64 copy and ordered by
 // (distance, index). Every candidate left out is bounded below: outside the
-// block by the block's reach, rejected against the first threshold by R^2,
-// rejected or evicted later by the (K+1)-th key V minus the f32 error. If
+// block by the block's reach, (list variant only) rejected against the first
+// threshold by R^2, rejected or evicted by the (K+1)-th key V minus the f32
+// error. If
 // that bound exceeds the K-th exact dsq (times 1 + 2^-46), the answer is
 // exact; otherwise the query goes to k_knn_slow with the K-th dsq as bound.
 template <int K>
