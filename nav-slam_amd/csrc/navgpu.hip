@@ -540,7 +540,10 @@ __device__ __forceinline__ void kd_node_range(int n, int depth, int k, int &lo, 
   }
 }
 
-constexpr int kLaneSubtree = 32;  // subarrays this short: one lane per subtree
+#ifndef NAVGPU_LANE_SUBTREE
+#define NAVGPU_LANE_SUBTREE 32
+#endif
+constexpr int kLaneSubtree = NAVGPU_LANE_SUBTREE;  // subarrays this short: one lane per subtree
 #ifndef NAVGPU_BLOCK_NTH_MIN
 #define NAVGPU_BLOCK_NTH_MIN 256
 #endif
