@@ -1257,16 +1257,6 @@ constexpr int kWPB = NAVGPU_KNNW_WPB;
 
 // inclusive wave64 prefix sum by DPP (row_shr 1/2/4/8, row_bcast 15/31):
 // every lane must be active
-__device__ __forceinline__ int wave_scan_add(int x) {
-  x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xf, 0xf, false);
-  x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xf, 0xf, false);
-  x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xf, 0xf, false);
-  x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xf, 0xf, false);
-  x += __builtin_amdgcn_update_dpp(0, x, 0x142, 0xa, 0xf, false);
-  x += __builtin_amdgcn_update_dpp(0, x, 0x143, 0xc, 0xf, false);
-  return x;
-}
-
 __device__ __forceinline__ int rdlane(int v, int l) { return __builtin_amdgcn_readlane(v, l); }
 
 // the f32 frame of a segment whose query cells are xf .. xl of row (y, z):

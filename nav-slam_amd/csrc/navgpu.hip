@@ -447,20 +447,19 @@ __device__ void block_nth_element(const double *key, IdxT *P, IdxT *T, int first
         bcn[b][wid] = __popcll(bal);
       }
       __syncthreads();
-      // the chunk's wave prefix (lane x of every wave: smalls in waves < x)
-      int c = lane < nw ? bcn[b][lane] : 0;
-      int incl = c;
-#pragma unroll
-      for (int o = 1; o <= NWM; o <<= 1) {  // lanes 0 .. NWM: up to 17 terms
-        const int t = __shfl_up(incl, o, kWave);
-        if (lane >= o) incl += t;
-      }
-      if (lane <= nw) bpre[wid][lane] = incl - c;  // lane nw: the chunk's total
-      wave_sync_mem();
-      const int before = bpre[wid][wid], tot = bpre[wid][nw];
+      // the chunk's wave prefix (lane x of every wave: smalls in waves < x;
+      // lane nw: the chunk's total), by DPP; this wave's own entries by
+      // readlane, the others' (for hops) through bpre
+      const int c = lane < nw ? bcn[b][lane] : 0;
+      const int excl = wave_scan_add(c) - c;
+      if (lane <= nw) bpre[wid][lane] = excl;
+      const int before = __builtin_amdgcn_readlane(excl, wid);
+      const int tot = __builtin_amdgcn_readlane(excl, nw);
       const int sp = S + before + lanes_below(bal);
       uint32_t w = (uint32_t)e;
-      if (small && sp != p) {
+      const bool hop = small && sp != p;
+      if (__any(hop)) wave_sync_mem();  // bpre before the hops read it
+      if (hop) {
         int y = tape_jump(p, sp, lbal & below, cs + wbase);
         for (;;) {
           if (y < cs) {
@@ -541,7 +540,7 @@ __device__ __forceinline__ void kd_node_range(int n, int depth, int k, int &lo, 
 }
 
 #ifndef NAVGPU_LANE_SUBTREE
-#define NAVGPU_LANE_SUBTREE 32
+#define NAVGPU_LANE_SUBTREE 16  // (r4: 32 -> 16, rows_probe --integer: build 593 -> 577 us)
 #endif
 constexpr int kLaneSubtree = NAVGPU_LANE_SUBTREE;  // subarrays this short: one lane per subtree
 #ifndef NAVGPU_BLOCK_NTH_MIN

@@ -120,6 +120,19 @@ __device__ __forceinline__ void wave_sync_mem() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 }
 
+// inclusive prefix sum over the 64 lanes by DPP (row shifts, then the row
+// broadcasts 15 and 31): no LDS, a few cycles per step
+__device__ __forceinline__ int wave_scan_add(int x) {
+  x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xf, 0xf, false);
+  x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xf, 0xf, false);
+  x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xf, 0xf, false);
+  x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xf, 0xf, false);
+  x += __builtin_amdgcn_update_dpp(0, x, 0x142, 0xa, 0xf, false);
+  x += __builtin_amdgcn_update_dpp(0, x, 0x143, 0xc, 0xf, false);
+  return x;
+}
+
+
 // Block-wide exclusive scan of one int per thread. scratch: >= nwaves+1 ints.
 __device__ __forceinline__ int block_excl_scan(int v, int *scratch, int *total) {
   const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
