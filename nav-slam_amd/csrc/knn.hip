@@ -459,7 +459,7 @@ __global__ __launch_bounds__(256) void k_bin_hist(BinJob J, const GridArgs A,
   grid_params_block(A, &sG);
   if (blockIdx.x == 0 && threadIdx.x < 16) counters[threadIdx.x] = 0;  // [4, 12): tickets
   __syncthreads();
-  const GridParams &G = sG;
+  const GridParams G = sG;  // (by value: registers, not an LDS read per point)
   if (blockIdx.x == 0 && threadIdx.x == 0) *gp = G;
   bin_chunk(S, blk, G, [&](int i, const P3 &, int c) {
     atomicAdd(&hist[c >> J.shift], 1);
