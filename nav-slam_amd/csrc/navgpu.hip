@@ -1981,7 +1981,7 @@ __global__ __launch_bounds__(NT) void k_rows_query_screen(
     const double *__restrict__ tree_pts, const int32_t *__restrict__ tree_n,
     const double *__restrict__ feat_src, const double *__restrict__ queries, int R, int C,
     int32_t *__restrict__ nn_pos, double *__restrict__ nn_dist, int32_t *__restrict__ mask_out,
-    int32_t *__restrict__ tie) {
+    int32_t *__restrict__ tie, const int32_t *__restrict__ tree_col) {
   const int r = blockIdx.x;
   const int w = (C + (int)gridDim.y - 1) / (int)gridDim.y;
   const int c0 = (int)blockIdx.y * w, c1 = min(C, c0 + w);
@@ -1997,6 +1997,10 @@ __global__ __launch_bounds__(NT) void k_rows_query_screen(
   uint16_t *FL = QL + align16(2 * w) / 2;
   int *scan = (int *)((unsigned char *)FL + align16(2 * w));
   uint32_t *stk = (uint32_t *)((unsigned char *)scan + align16(4 * 40));
+  // lazy rows (column order, no tree): the walk stack's region holds the
+  // rows' feature columns instead (no query walks here)
+  uint16_t *TCOL = (uint16_t *)stk;
+  const bool lazy = tree_col != nullptr;
   const int n = tree_n[r];
   const int nch = (n + kScreenChunk - 1) / kScreenChunk;
   for (int pos = threadIdx.x; pos < nch * kScreenChunk; pos += NT) {
@@ -2005,6 +2009,7 @@ __global__ __launch_bounds__(NT) void k_rows_query_screen(
       TX[pos] = t[0];
       TY[pos] = t[1];
       TZ[pos] = t[2];
+      if (lazy) TCOL[pos] = (uint16_t)tree_col[rowoff + pos];
     } else {
       TX[pos] = TY[pos] = TZ[pos] = INFINITY;  // dsq = inf: never taken
     }
@@ -2044,7 +2049,23 @@ __global__ __launch_bounds__(NT) void k_rows_query_screen(
     // starts empty, so no point is counted twice (a point counted twice would
     // look like a runner-up at the minimum's distance).
     double e1 = INFINITY, e2 = INFINITY;
-    {
+    // lazy rows: the scan starts at the chunks holding the first feature at or
+    // after the wave's first query column (a scan row is an azimuth sweep)
+    int s0 = -1, s1 = -1;
+    if (lazy && nch > 0) {
+      const int q0 = QL[i0];
+      int lo = 0, hi = n;  // lower bound of q0 in the row's sorted columns
+      while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if ((int)TCOL[mid] < q0)
+          lo = mid + 1;
+        else
+          hi = mid;
+      }
+      s0 = __builtin_amdgcn_readfirstlane(min(lo / kScreenChunk, nch - 1));
+      s1 = min(s0 + 1, nch - 1);
+    }
+    if (!lazy) {
       int a0 = 0, a1 = n, depth = 0;
       while (a0 < a1) {
         const int mid = a0 + ((a1 - a0) >> 1);
@@ -2071,7 +2092,7 @@ __global__ __launch_bounds__(NT) void k_rows_query_screen(
     }
     double d1 = INFINITY, d2 = INFINITY;
     int j1 = -1;
-    screen_query(T, act, qx, qy, qz, -1, -1, d1, d2, j1, e2);
+    screen_query(T, act, qx, qy, qz, s0, s1, d1, d2, j1, e2);
     const double dist = __builtin_sqrt(d1);
     bool genuine;
     int emin;
@@ -3233,7 +3254,8 @@ static int rows_query_launch(navgpu_ctx *ctx, const double *tree_pts,
                              const int32_t *tree_n, const double *feat_src,
                              const double *queries, int R, int C,
                              int32_t *nn_pos, double *nn_dist,
-                             int32_t *mask_out, int32_t *tie) {
+                             int32_t *mask_out, int32_t *tie,
+                             const int32_t *tree_col = nullptr) {
   ARG_CHECK(ctx);
   RC(check_rows_shape(R, C, true));
   if ((size_t)R * C == 0) return NAVGPU_OK;
@@ -3246,9 +3268,10 @@ static int rows_query_launch(navgpu_ctx *ctx, const double *tree_pts,
     while (S < 16 && (long long)R * S < 1024 && C / (2 * S) >= 128) S <<= 1;
     const int w = (C + S - 1) / S;
     const int cp = (C + kScreenChunk - 1) / kScreenChunk * kScreenChunk;
+    // (the last region: the walk stacks, or the lazy rows' feature columns)
     const int lds = 3 * align16(8 * cp) + align16(48 * (cp / kScreenChunk)) +
                     align16(24 * (w + 4)) + 2 * align16(2 * w) + align16(4 * 40) +
-                    4 * kRowsQBlock * kStackDepth;
+                    std::max(4 * kRowsQBlock * kStackDepth, align16(2 * C));
     if (lds > lds_limit()) {
       set_err("rows_query: C=%d needs %d B of LDS (device limit %d)", C, lds, lds_limit());
       return NAVGPU_ERANGE;
@@ -3257,7 +3280,7 @@ static int rows_query_launch(navgpu_ctx *ctx, const double *tree_pts,
     TimedRegion tr(ctx, "rows_query");
     hipLaunchKernelGGL(k_rows_query_screen<kRowsQBlock>, dim3(R, S), dim3(kRowsQBlock), lds,
                        ctx->stream, tree_pts, tree_n, feat_src, queries, R, C, nn_pos, nn_dist,
-                       mask_out, tie);
+                       mask_out, tie, tie ? tree_col : nullptr);
     CHECK_LAUNCH("k_rows_query_screen");
     return NAVGPU_OK;
   }
@@ -3301,7 +3324,7 @@ int navgpu_kd_query_rows_lazy_dev(navgpu_ctx *ctx, double *tree_pts, int32_t *tr
   RC(ws(ctx, kRowTie, (size_t)R, &tie));
   HIP_TRY(hipMemsetAsync(tie, 0, 4 * (size_t)R, ctx->stream));
   RC(rows_query_launch(ctx, tree_pts, tree_n, feat_src, queries, R, C, nn_pos, nn_dist,
-                       mask_out, tie));
+                       mask_out, tie, tree_col));
   const RowsLds L = rows_lds(C, kRowsBlock, true);
   if (L.total > lds_limit()) {
     set_err("rows_query_lazy: C=%d needs %d B of LDS (device limit %d)", C, L.total,
