@@ -1,6 +1,6 @@
 #!/bin/bash
-# r4 final check: the whole GPU suite, smoke, the default bench line
-TAG=${1:-r4final}; OUT=gpurun_out/$TAG; mkdir -p "$OUT"
+# Final check: the whole GPU suite, smoke, the default bench line
+TAG=${1:-final}; OUT=gpurun_out/$TAG; mkdir -p "$OUT"
 export NAVSLAM_QUIET=1 PYTHONUNBUFFERED=1
 timeout -k 10 700 python3 -u -m pytest tests -m gpu -x -v --timeout 240 --timeout-method thread \
   > "$OUT/pytest.log" 2>&1; rc=$?

@@ -1,7 +1,7 @@
 #!/bin/bash
-# r4: K3 k_knnw knobs: grid occupancy / x slicing (env), records per wave and
+# K3 k_knnw knobs: grid occupancy / x slicing (env), records per wave and
 # register budget (variant builds); knn_probe query_us / build_us
-TAG=${1:-r4s13}; OUT=gpurun_out/$TAG; mkdir -p "$OUT"
+TAG=${1:-knn_knobs}; OUT=gpurun_out/$TAG; mkdir -p "$OUT"
 export NAVSLAM_QUIET=1 PYTHONUNBUFFERED=1 NAVGPU_KNN_STATS=1
 V=nav-slam_amd/lib/variants
 p() {  # p <label> <lib> [VAR=value ...]

@@ -1,7 +1,7 @@
 #!/bin/bash
-# r4: per-row build variants (lane-subtree cutoff, block levels down to 256)
+# Per-row build variants (lane-subtree cutoff, block levels down to 256)
 # on integer-mm K2 rows (stamps builds), then K2 with 256-thread screen blocks
-TAG=${1:-r4s16}; OUT=gpurun_out/$TAG; mkdir -p "$OUT"
+TAG=${1:-rows_build}; OUT=gpurun_out/$TAG; mkdir -p "$OUT"
 export NAVSLAM_QUIET=1 PYTHONUNBUFFERED=1
 for r in 1 2; do for l in st st_l16 st_b256 st_l16b256; do
   timeout -k 10 120 python3 scripts/rows_probe.py --integer --lib nav-slam_amd/lib/var_st/libnavgpu_$l.so \

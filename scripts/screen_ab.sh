@@ -1,7 +1,7 @@
 #!/bin/bash
-# r4: the f32 screen with fused curvature: row tests, then K4 / K2 fused vs
+# The f32 screen with fused curvature: row tests, then K4 / K2 fused vs
 # unfused vs f64, K4 with 256-thread screen blocks
-TAG=${1:-r4s12}; OUT=gpurun_out/$TAG; mkdir -p "$OUT"
+TAG=${1:-screen_ab}; OUT=gpurun_out/$TAG; mkdir -p "$OUT"
 export NAVSLAM_QUIET=1 PYTHONUNBUFFERED=1
 timeout -k 10 400 python3 -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread \
   -k "rows or screen or lazy or smoke or shim or bench" > "$OUT/pytest.log" 2>&1; rc=$?
