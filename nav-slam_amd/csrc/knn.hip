@@ -1245,7 +1245,10 @@ constexpr int kWRec = NAVGPU_KNNW_REC;   // staged records per wave (16 B each)
 constexpr int kWPairs = kWRec / 2 + 2;   // two spare pairs: read-ahead
 constexpr int kWZg = 4 * kWPairs;        // floats from the XY plane to the ZG plane
 constexpr int kWCols = 2 * kWave;        // staged columns per round: two per lane
-constexpr int kWSegs = 8;                // segments (grid rows) per round
+#ifndef NAVGPU_KNNW_SEGS
+#define NAVGPU_KNNW_SEGS 8
+#endif
+constexpr int kWSegs = NAVGPU_KNNW_SEGS;  // segments (grid rows) per round
 // waves per workgroup, each with its own chunk and LDS region
 #ifndef NAVGPU_KNNW_WPB
 #define NAVGPU_KNNW_WPB 1
