@@ -48,6 +48,7 @@ extern "C" {
 #define NAVGPU_EHIP (-2)    /* HIP runtime error (no device, fault, ...) */
 #define NAVGPU_ENOMEM (-3)  /* device allocation failed                   */
 #define NAVGPU_ERANGE (-4)  /* shape beyond what a kernel supports        */
+#define NAVGPU_EINTERNAL (-5) /* a kernel met an out-of-range index (bug)  */
 
 typedef struct navgpu_ctx navgpu_ctx;
 
@@ -286,6 +287,12 @@ long long navgpu_knn_fallbacks(navgpu_ctx *ctx);
 /* Diagnostic: k_knn tiles of the last navgpu_knn_* call whose neighbourhood
  * exceeded the LDS tile budget and ran from global memory (synchronises). */
 long long navgpu_knn_overflows(navgpu_ctx *ctx);
+/* Integrity check of the last navgpu_knn_* / navgpu_pair_knn_dev call
+ * (synchronises): NAVGPU_EINTERNAL when a k-NN kernel met a list, cloud or
+ * record index out of range (it clamps the address so the device cannot
+ * fault, and flags the call); NAVGPU_OK otherwise. navgpu_knn_host checks
+ * it itself. */
+int navgpu_knn_check(navgpu_ctx *ctx);
 /* Diagnostic: rows of the last navgpu_rows_match_* call that had a query
  * with a distance tie and so ran the reference tree (synchronises); -1 when
  * the last call did not screen (NAVGPU_ROWS_SCREEN=0) or none was made. */

@@ -54,6 +54,8 @@ struct GridParams {
   int tile_w;             // query cells (x) per k_knn tile
   int clamped;            // some axis hit the 2048-cell cap: its boundary cells
                           // hold points beyond their nominal box
+  double c[3];            // (r5) the grid's centre: the one f32 frame of k_knng
+  double Dt;              // bound on |t - c| per axis for every target (slack included)
 };
 
 // one point of a cell-sorted cloud: the caller's f64 coordinates, its index
@@ -213,6 +215,8 @@ __device__ void grid_params_block(const GridArgs A, GridParams *out) {
     G.ncells = 1;
     G.tile_w = 1;
     G.clamped = 0;
+    for (int a = 0; a < 3; ++a) G.c[a] = 0.5;
+    G.Dt = 1.0;
     *out = G;
     return;
   }
@@ -253,6 +257,15 @@ __device__ void grid_params_block(const GridArgs A, GridParams *out) {
   G.g[1] = g[1];
   G.g[2] = g[2];
   G.ncells = g[0] * g[1] * g[2];
+  // the grid's centre, and a bound on |t - c| for every target: the bbox
+  // [lo, lo + ext] lies in [o, o + g e] unless an axis was clamped, and in
+  // [o, o + emax] always
+  double half = 0.0;
+  for (int a = 0; a < 3; ++a) {
+    G.c[a] = G.o[a] + 0.5 * (g[a] * G.e[a]);
+    half = fmax(half, 0.5 * (g[a] * G.e[a]));
+  }
+  G.Dt = (clamped ? fmax(half, emax) : half) + 4.0 * G.delta;
   // tile width: ~kTileQueries queries per tile, and its 9 staged row
   // segments of W + 2 sx cells within ~90 % of the LDS record budget;
   // balanced: the fewest tiles per grid row at that width, then equal widths
@@ -281,6 +294,16 @@ __device__ __forceinline__ int cell_of(const double *p, const GridParams &G) {
 
 constexpr int kBinMaxBuckets = 4096;  // coarse buckets per side (k_bin_*)
 
+// (r5) Lean build kernels: 256-thread blocks of at most 64 VGPRs and a few KB
+// of LDS, so that with two pairs in flight each of them fits on a CU beside
+// the other pair's query pass (k_knng: 3 waves per SIMD of 147 VGPRs, 115 KB
+// of LDS per CU) instead of waiting for it to drain.
+#ifndef NAVGPU_BUILD_LEAN
+#define NAVGPU_BUILD_LEAN 0
+#endif
+constexpr bool kLean = NAVGPU_BUILD_LEAN;
+constexpr int kBuildMinW = kLean ? 8 : 1;  // launch-bounds waves per SIMD (8: <= 64 VGPRs)
+
 // ---- (bucket, block) offsets of the binning (k_bin_*) ---------------------
 // The count table is block-major per side, T[tab + blk * nb + b], so that
 // k_bin_hist writes and k_bin_scatter reads one contiguous row per block.
@@ -289,9 +312,10 @@ constexpr int kBinMaxBuckets = 4096;  // coarse buckets per side (k_bin_*)
 // (the exclusive scan of btot) are recomputed in LDS by every k_bin_scatter
 // block (cheaper than a one-block launch); block 0 of each side publishes them
 // to bbase[side * (nb + 1) + 0 .. nb] for k_bin_fine.
-constexpr int kColB = 64;              // buckets per k_bin_colscan block
+constexpr int kColB = kLean ? 16 : 64;  // buckets per k_bin_colscan block
 constexpr int kColY = 16;              // block-row chunks per bucket column
-__global__ __launch_bounds__(kColB * kColY) void k_bin_colscan(int *__restrict__ T, int nb,
+constexpr int kColU = kLean ? 8 : 16;  // loads in flight per thread
+__global__ __launch_bounds__(kColB * kColY, kBuildMinW) void k_bin_colscan(int *__restrict__ T, int nb,
                                                                int tab0, int nblk0, int tab1,
                                                                int nblk1, int *__restrict__ btot) {
   __shared__ int part[kColY][kColB];
@@ -303,7 +327,7 @@ __global__ __launch_bounds__(kColB * kColY) void k_bin_colscan(int *__restrict__
   const int ch = (nblk + kColY - 1) / kColY;
   const int k0 = min(nblk, y * ch), k1 = min(nblk, k0 + ch);
   // a chunk's counts: every load in flight before any is used
-  constexpr int U = 16;
+  constexpr int U = kColU;
   int v[U], sum = 0;
   for (int k = k0; k < k1; k += U) {
 #pragma unroll
@@ -395,9 +419,34 @@ __device__ __forceinline__ BinPt qload(const QSide &QS, int pos) {
 struct BinJob {
   BinSide s[2];
   int shift, nb;  // buckets per side
+  int sglobal;    // SRec form: 1 = k_knng's (grid-centre frame + position), 0 = k_knnw's
 };
+
+// the SRec of the target at cell-sorted position pos: k_knng reads f32
+// offsets from the grid centre and the record's position (its image needs no
+// per-record shift: DESIGN.md §4 r5); k_knnw the offset from the record's own
+// cell centre and its x column
+__device__ __forceinline__ SRec make_srec(const GridParams &G, bool sglobal, double x, double y,
+                                          double z, int cell, int pos) {
+  SRec r;
+  if (sglobal) {
+    r.x = (float)(x - G.c[0]);
+    r.y = (float)(y - G.c[1]);
+    r.z = (float)(z - G.c[2]);
+    r.cx = pos;
+    return r;
+  }
+  const int g0 = G.g[0], g1 = G.g[1];
+  const int row = cell / g0, cx = cell - row * g0;
+  const int cy = row % g1, cz = row / g1;
+  r.x = (float)(x - (G.o[0] + (cx + 0.5) * G.e[0]));
+  r.y = (float)(y - (G.o[1] + (cy + 0.5) * G.e[1]));
+  r.z = (float)(z - (G.o[2] + (cz + 0.5) * G.e[2]));
+  r.cx = cx;
+  return r;
+}
 constexpr int kBinMaxShift = 15;
-constexpr int kBinUnroll = 8;  // points per thread with loads in flight
+constexpr int kBinUnroll = kLean ? 4 : 8;  // points per thread with loads in flight
 // (compile-time knobs for A/B variant builds, scripts/build_variants.sh)
 #ifndef NAVGPU_BIN_P
 #define NAVGPU_BIN_P 4096
@@ -406,12 +455,12 @@ constexpr int kBinUnroll = 8;  // points per thread with loads in flight
 #define NAVGPU_BIN_MIN_SHIFT 10
 #endif
 #ifndef NAVGPU_BIN_FINE_THREADS
-#define NAVGPU_BIN_FINE_THREADS 512
+#define NAVGPU_BIN_FINE_THREADS (NAVGPU_BUILD_LEAN ? 256 : 512)
 #endif
 constexpr int kBinP = NAVGPU_BIN_P;  // minimum points per k_bin_hist / k_bin_scatter block
 constexpr int kBinMinShift = NAVGPU_BIN_MIN_SHIFT;  // coarse buckets of 2^10 cells (r2 A/B)
 constexpr int kBinFineThreads = NAVGPU_BIN_FINE_THREADS;
-constexpr int kBinFineHold = 4096 / kBinFineThreads;  // points per thread held in registers
+constexpr int kBinFineHold = kLean ? 2 : 4096 / kBinFineThreads;  // points per thread held in registers
 
 __device__ __forceinline__ int bin_side(const BinJob &J, int &blk) {
   const int side = blk >= J.s[0].nblk ? 1 : 0;
@@ -447,11 +496,11 @@ __device__ __forceinline__ void bin_chunk(const BinSide &S, int blk, const GridP
 // Also derives the grid (grid_params_block; block 0 publishes it to *gp and
 // resets the call's k-NN counters) and keeps each query's cell for
 // k_bin_scatter (4 B instead of re-reading its 24-B point).
-__global__ __launch_bounds__(256) void k_bin_hist(BinJob J, const GridArgs A,
+__global__ __launch_bounds__(256, kBuildMinW) void k_bin_hist(BinJob J, const GridArgs A,
                                                   GridParams *__restrict__ gp,
                                                   int *__restrict__ counters,
                                                   int *__restrict__ table) {
-  __shared__ int hist[kBinMaxBuckets];
+  extern __shared__ int hist[];  // J.nb counters
   __shared__ GridParams sG;
   int blk = blockIdx.x;
   const BinSide S = J.s[bin_side(J, blk)];
@@ -469,11 +518,11 @@ __global__ __launch_bounds__(256) void k_bin_hist(BinJob J, const GridArgs A,
   for (int b = threadIdx.x; b < J.nb; b += blockDim.x) table[S.tab + blk * J.nb + b] = hist[b];
 }
 
-__global__ __launch_bounds__(256) void k_bin_scatter(BinJob J, const GridParams *__restrict__ gp,
+__global__ __launch_bounds__(256, kBuildMinW) void k_bin_scatter(BinJob J, const GridParams *__restrict__ gp,
                                                      const int *__restrict__ offs,
                                                      const int *__restrict__ btot,
                                                      int *__restrict__ bbase) {
-  __shared__ int cur[kBinMaxBuckets];
+  extern __shared__ int cur[];  // J.nb cursors
   __shared__ int scratch[40];
   int blk = blockIdx.x;
   const int side = bin_side(J, blk);
@@ -551,7 +600,7 @@ constexpr int kFineStageHold = kFineStage / kBinFineThreads;
 constexpr size_t fine_lds_bytes(int shift, bool stage_q) {
   return ((size_t)4 << shift) + (stage_q ? (size_t)kFineStage * sizeof(uint16_t) : 0);
 }
-__global__ __launch_bounds__(kBinFineThreads) void k_bin_fine(BinJob J,
+__global__ __launch_bounds__(kBinFineThreads, kBuildMinW) void k_bin_fine(BinJob J,
                                                               const GridParams *__restrict__ gp,
                                                               const int *__restrict__ bbase,
                                                               int nscan, int qstage) {
@@ -625,7 +674,7 @@ __global__ __launch_bounds__(kBinFineThreads) void k_bin_fine(BinJob J,
   }
   __syncthreads();
   const GridParams &G = *gp;
-  const int g0 = G.g[0], g1 = G.g[1];
+  const int g0 = G.g[0];
   if (staged) {
 #pragma unroll
     for (int u = 0; u < kFineStageHold; ++u) {
@@ -650,13 +699,7 @@ __global__ __launch_bounds__(kBinFineThreads) void k_bin_fine(BinJob J,
         const int row = e.cell / g0;
         t.cx = e.cell - row * g0;
         S.sorted[lo + j] = t;
-        const int cy = row % g1, cz = row / g1;
-        SRec r;
-        r.x = (float)(e.x - (G.o[0] + (t.cx + 0.5) * G.e[0]));
-        r.y = (float)(e.y - (G.o[1] + (cy + 0.5) * G.e[1]));
-        r.z = (float)(e.z - (G.o[2] + (cz + 0.5) * G.e[2]));
-        r.cx = t.cx;
-        S.srec[lo + j] = r;
+        S.srec[lo + j] = make_srec(G, J.sglobal, e.x, e.y, e.z, e.cell, lo + j);
       }
     }
     return;
@@ -675,15 +718,7 @@ __global__ __launch_bounds__(kBinFineThreads) void k_bin_fine(BinJob J,
       const int row = e.cell / g0;
       t.cx = e.cell - row * g0;
       S.sorted[pos] = t;
-      // offsets from the f64 cell centre (k_knnw adds the centre's shift
-      // into its frame: DESIGN.md §4, SRec)
-      const int cy = row % g1, cz = row / g1;
-      SRec r;
-      r.x = (float)(e.x - (G.o[0] + (t.cx + 0.5) * G.e[0]));
-      r.y = (float)(e.y - (G.o[1] + (cy + 0.5) * G.e[1]));
-      r.z = (float)(e.z - (G.o[2] + (cz + 0.5) * G.e[2]));
-      r.cx = t.cx;
-      S.srec[pos] = r;
+      S.srec[pos] = make_srec(G, J.sglobal, e.x, e.y, e.z, e.cell, pos);
     }
   };
 #pragma unroll
@@ -700,6 +735,92 @@ __global__ __launch_bounds__(kBinFineThreads) void k_bin_fine(BinJob J,
     } else {
       place(src[i], i);
     }
+  }
+}
+
+// ---- (r5) the row neighbourhood lists k_knng stages from -------------------
+// For grid row R = (y, z), its list GL_R holds, column by column (x = 0 ..
+// g0-1), the cell-sorted positions of the targets of the 9 cells (x, y+dy,
+// z+dz), dy, dz in {-1, 0, 1} in the order s = 3 (dz+1) + (dy+1), each cell's
+// run in order. A query in cell (x, R) then finds its whole block (cells
+// x-sx .. x+sx of the 9 rows) as ONE contiguous range of GL_R, and a run of
+// query cells of one row stages ONE contiguous slice.
+//
+// Where GL_R starts needs no scan. Pad the (y, z) plane with one empty row of
+// cells on every side and number the padded rows P in the grid's order; every
+// padded row gets the list of its 9 neighbours, and the lists lie in P order.
+// Row P's 9 neighbours are P + sigma_s (sigma_s = dz (g1+2) + dy, no wrap can
+// reach a non-empty row), so the targets in the lists before P's number
+// sum_s C(P + sigma_s), C(Q) = the targets in real rows before padded row Q,
+// which is tstart at that row's first cell (0 below the grid, nt above it, a
+// z slab's start or end beside it). Within the row, column x starts after
+// tstart[(R_s) g0 + x] - tstart[(R_s) g0] more of each neighbour R_s, so
+//   npg(R, x) = sum_s T_s(x),  T_s(x) = tstart[(y+dy, z+dz) g0 + x] for an
+//   in-grid neighbour, C(P + sigma_s) otherwise,
+// and the lists take exactly 9 nt positions. npg is stored per row with g0+1
+// entries (x = g0: the row's end; rows are not adjacent in the padded order).
+// One thread per (row, x): 18 tstart loads (L2), the npg entry and the
+// column's ~9 occ positions written in order.
+__device__ __forceinline__ int nb_pos(int yy, int zz, int x, int g0, int g1, int g2, int &real) {
+  real = 0;
+  if (zz < 0) return 0;                              // tstart[0] = 0
+  if (zz >= g2) return g0 * g1 * g2;                 // = nt
+  if (yy < 0) return zz * g1 * g0;                   // the slab's start
+  if (yy >= g1) return (zz + 1) * g1 * g0;           // its end
+  real = 1;
+  return (zz * g1 + yy) * g0 + x;
+}
+
+// One WAVE per task = 64 consecutive columns of one row: lane = column for the
+// loads and npg, then lane = (column, s) cell run for the list writes, so one
+// store instruction covers 64 consecutive runs (a few cache lines) instead of
+// 64 columns ~15 positions apart.
+constexpr int kNbWaves = 4;  // waves per k_nb_fill workgroup
+__global__ __launch_bounds__(kWave * kNbWaves) void k_nb_fill(const GridParams *__restrict__ gp,
+                                                              const int *__restrict__ tstart,
+                                                              int *__restrict__ npg,
+                                                              int *__restrict__ gl) {
+  __shared__ int tab[kNbWaves][2][kWave * 9 + 1];  // per (column, s): start, list offset
+  const int g0 = gp->g[0], g1 = gp->g[1], g2 = gp->g[2];
+  const int w = g0 + 1;
+  const int tpr = (w + kWave - 1) / kWave;  // tasks per row
+  const int ntask = g1 * g2 * tpr;
+  const int wid = (int)threadIdx.x / kWave, lane = (int)threadIdx.x & (kWave - 1);
+  int *ta = tab[wid][0], *to = tab[wid][1];  // run r's count: to[r + 1] - to[r]
+  for (int t = blockIdx.x * kNbWaves + wid; t < ntask; t += gridDim.x * kNbWaves) {
+    const int R = t / tpr, x0 = (t - R * tpr) * kWave;
+    const int y = R % g1, z = R / g1;
+    const int x = x0 + lane;
+    const int xc = min(x, g0);
+    int a[9], c[9], base = 0;
+#pragma unroll
+    for (int s = 0; s < 9; ++s) {
+      int real;
+      const int p = nb_pos(y + s % 3 - 1, z + s / 3 - 1, xc, g0, g1, g2, real);
+      // both loads unconditional (a branch per load would wait for each)
+      const int va = tstart[p];
+      const int vb = tstart[real && xc < g0 ? p + 1 : p];
+      a[s] = va;
+      c[s] = x < g0 ? vb - va : 0;
+      base += va;
+    }
+    if (x <= g0) npg[R * w + x] = base;
+    int off = base;
+#pragma unroll
+    for (int s = 0; s < 9; ++s) {
+      ta[lane * 9 + s] = a[s];
+      to[lane * 9 + s] = off;
+      off += c[s];
+    }
+    if (lane == kWave - 1) to[kWave * 9] = off;
+    wave_sync_mem();
+#pragma unroll
+    for (int it = 0; it < 9; ++it) {
+      const int r = it * kWave + lane;
+      const int va = ta[r], o = to[r], n = to[r + 1] - o;
+      for (int k = 0; k < n; ++k) gl[o + k] = va + k;
+    }
+    wave_sync_mem();  // the tables are rewritten by the wave's next task
   }
 }
 
@@ -764,6 +885,7 @@ struct KnnLists {
   int *slow_q, *n_slow;  // queries (cell-sorted positions) the fast path could not certify
   double *slow_thr;      // their starting bound (K-th dsq upper bound), or inf
   int *n_unstaged;       // of them: queries whose block exceeded the LDS budget
+  int *err;              // set when a kernel had to clamp an index (navgpu_knn_check)
   int vec_out;           // outputs 16-B aligned: results may be stored as vectors
 };
 
@@ -1797,6 +1919,369 @@ __global__ __launch_bounds__(kWave * kWPB, NAVGPU_KNNW_MINW) void k_knnw(const G
   NV_WFLUSH(chunk);
 }
 
+// ============================================================ k_knng
+// The query pass on the row neighbourhood lists (r5, default): one WAVE per
+// chunk of 64 consecutive cell-sorted queries, as k_knnw, but with no column
+// tables, no per-segment frames and no per-record shift or shuffle:
+//  * a lane's block is [npg(R, x - sx), npg(R, x + sx + 1)) of its row's list
+//    GL_R (k_nb_fill): two loads;
+//  * the chunk's queries fall in a few grid rows (segments); a segment's
+//    image is ONE slice of its row's list, so the round's LDS image is the
+//    concatenation of the segments' slices: slot j holds gl[j + delta], delta
+//    per segment; every position and record load of the round is in flight
+//    at once (kGU batches), then each record is written to its slot with its
+//    cell-sorted position (the exact stage reads the K best positions there);
+//  * every record is an f32 offset from ONE frame, the grid centre c (SRec,
+//    k_bin_fine), so staging copies it as it is; each coordinate difference
+//    is still within dl = Dq 2^-21 of the exact one with Dq >= |t - c|,
+//    |q - c| (G.Dt), only Dq is larger than a segment frame's.
+// The scan, exact stage and certificate are k_knnw's.
+// Indices are checked where they are clamped: a position outside the list or
+// the cloud sets the call's error flag (navgpu_knn_check returns
+// NAVGPU_EINTERNAL).
+#ifndef NAVGPU_KNNG_REC
+#define NAVGPU_KNNG_REC 800
+#endif
+#ifndef NAVGPU_KNNG_MINW
+#define NAVGPU_KNNG_MINW 3
+#endif
+// 3 waves per SIMD: 4 (<= 128 VGPRs) spills, and more waves only lengthen
+// every wave's memory round trips (r5 timeline)
+constexpr int kGRec = NAVGPU_KNNG_REC;          // staged records per round (16 B each)
+constexpr int kGPairs = kGRec / 2 + 2;          // two spare pairs: read-ahead
+constexpr int kGZg = 4 * kGPairs;               // floats from the XY plane to the ZG plane
+constexpr int kGU = (kGRec + kWave - 1) / kWave;  // staging batches of a full round
+
+#ifdef NAVGPU_STAMPS
+// k_knng's per-chunk timeline (stamps builds only): [0] start, [1] end
+// (s_memrealtime, 100 MHz, one clock for the chip), [2] HW_ID, [3] XCC_ID,
+// [4] staging, [5] scan, [6] exact stage (s_memtime cycles), [7] rounds
+constexpr int kGStampChunks = 1 << 15;
+__device__ unsigned long long g_gstamps[kGStampChunks][8];
+#define NV_GT(v) const unsigned long long v = __builtin_amdgcn_s_memtime()
+#define NV_GADD(i, a, b) gst[i] += (b) - (a)
+#else
+#define NV_GT(v)
+#define NV_GADD(i, a, b)
+#endif
+
+struct F3 {
+  float x, y, z;
+};
+
+template <int K>
+__global__ __launch_bounds__(kWave, NAVGPU_KNNG_MINW) void k_knng(
+    const GridParams *__restrict__ gp, const int *__restrict__ npg, const int *__restrict__ gl,
+    int ngl, const PRec *__restrict__ tsort, const SRec *__restrict__ srec, const QSide QS,
+    int nq, int ntg, int32_t *__restrict__ oidx, double *__restrict__ odist, KnnLists L_) {
+  // the round's image: an XY plane (x0 x1 y0 y1 per pair of slots) and a ZG
+  // plane (z0 z1 g0 g1, g = the cell-sorted position)
+  __shared__ __attribute__((aligned(16))) float spair[2 * kGZg];
+  constexpr int KL = K + 1;
+  static_assert(K >= 1 && K <= 16, "K");
+  const GridParams G = *gp;
+  const int S = G.sx, g0 = G.g[0], g1 = G.g[1];
+  // chunks dealt to the 8 XCDs in contiguous ranges (block b -> XCD b % 8)
+  const int nchunk = (nq + kWave - 1) / kWave;
+  const int per = (nchunk + 7) / 8;
+  const int cx = (int)(blockIdx.x >> 3);
+  const int chunk = (int)(blockIdx.x & 7) * per + cx;
+  if (cx >= per || chunk >= nchunk) return;
+  const int lane = (int)threadIdx.x;
+#ifdef NAVGPU_STAMPS
+  unsigned long long gst[8] = {__builtin_amdgcn_s_memrealtime(), 0, 0, 0, 0, 0, 0, 0};
+#endif
+  const int nlive = min(kWave, nq - chunk * kWave);
+  const int qi = chunk * kWave + lane;
+  const bool live = lane < nlive;
+  const int qc = min(qi, nq - 1);
+  const int qcell = QS.cell[qc];
+  const int qidx = QS.idx[qc];
+  // the query's cell: x, row = (z g1 + y); rows ascend over the lanes
+  const int qrow = live ? qcell / g0 : 0x7fffffff;
+  const int qx = live ? qcell - qrow * g0 : 0;
+  const int rs = live ? qrow * (g0 + 1) : 0;
+  // the lane's block in its row's list (k_nb_fill), then its point (f64;
+  // issued after the block so the first wait does not cover it). (Cell-sorted
+  // query records written by k_bin_fine were measured in r5: the query pass
+  // 142 -> 138 us, but the build's gather of the points 115 -> 147 us.)
+  const int ga = npg[rs + max(qx - S, 0)];
+  const int gb = npg[rs + min(qx + S + 1, g0)];
+  const double *qp = QS.pts + 3 * (size_t)qidx;
+  const double qv[3] = {qp[0], qp[1], qp[2]};
+  const uint32_t vmask = ~kKeyMask;
+  int bad = 0;  // an index that had to be clamped (a logic error)
+  const int prow = __shfl_up(qrow, 1, kWave), nrow = __shfl_down(qrow, 1, kWave);
+  const unsigned long long rowfirst = __ballot(live && (lane == 0 || prow != qrow));
+  const unsigned long long rowlast = __ballot(live && (lane == nlive - 1 || nrow != qrow));
+  for (int la = 0; la < nlive;) {
+    // ---- segments of lanes [la, nlive): a grid row each (the first one may
+    // start mid-row after a cut round)
+    const bool in = lane >= la && live;
+    const unsigned long long fall = (rowfirst & (~0ull << la)) | (1ull << la);
+    const unsigned long long below = (2ull << lane) - 1;  // lanes <= lane (lane 63: all)
+    const int sf = 63 - __builtin_clzll((fall & below) | 1ull);  // the lane's segment: first lane
+    const int sl = (int)__builtin_ctzll((rowlast & ~(below >> 1)) | (1ull << 63));  // ... last
+    const bool first = in && sf == lane, last = in && sl == lane;
+    const int A = __shfl(ga, sf, kWave);       // the segment's first list position
+    const int val = last ? gb - A : 0;         // a segment's slots, at its last lane
+    const int incv = wave_scan_add(val);
+    const int pre = in ? incv - val : 0;       // slots of the earlier segments
+    const int cum = pre + (gb - A);            // slots if the round ended at this lane
+    // the round: the lane prefix whose image fits (cum ascends over the lanes)
+    const int lb = la + __popcll(__ballot(in && cum <= kGRec));
+    if (lb == la) {
+      // lane la's block alone exceeds the budget: it and every lane of its
+      // cell (the same block) go to k_knn_slow from an infinite bound
+      const bool same = in && qcell == rdlane(qcell, la);
+      if (same) {
+        push_slow(L_, qi, INFINITY);
+        atomicAdd(L_.n_unstaged, 1);
+      }
+      la += __popcll(__ballot(same));
+      continue;
+    }
+    const int total = rdlane(cum, lb - 1);
+    NV_GT(ts0);
+    if (total > 0) {
+      // ---- staging: slot j of the round holds gl[j + delta(segment of j)]
+      const unsigned long long fb = __ballot(first && lane < lb);
+      int dl_[kGU];
+      {
+        const int f0 = (int)__builtin_ctzll(fb);
+        const int d0 = rdlane(A - pre, f0);
+#pragma unroll
+        for (int u = 0; u < kGU; ++u) dl_[u] = d0;
+        for (unsigned long long b = fb & (fb - 1); b; b &= b - 1) {
+          const int f = (int)__builtin_ctzll(b);
+          const int pf = rdlane(pre, f), df = rdlane(A - pre, f);
+#pragma unroll
+          for (int u = 0; u < kGU; ++u) dl_[u] = u * kWave + lane >= pf ? df : dl_[u];
+        }
+      }
+      // every load of the round issued unconditionally from a clamped index
+      // (a per-element condition makes hipcc branch around each load and wait
+      // for it); slots past the image discard theirs, a clamp inside it is
+      // an error (flagged)
+      int gpos[kGU];
+#pragma unroll
+      for (int u = 0; u < kGU; ++u) {
+        const int j = u * kWave + lane;
+        const int gi = min(j, total - 1) + dl_[u];
+        bad |= (unsigned)gi >= (unsigned)ngl;
+        gpos[u] = gl[min(max(gi, 0), ngl - 1)];
+      }
+      F3 rec[kGU];  // (12 of the record's 16 B: one dwordx3 each)
+#pragma unroll
+      for (int u = 0; u < kGU; ++u) {
+        bad |= (unsigned)gpos[u] >= (unsigned)ntg;
+        rec[u] = *(const F3 *)&srec[min(max(gpos[u], 0), ntg - 1)];
+      }
+#pragma unroll
+      for (int u = 0; u < kGU; ++u) {
+        const int j = u * kWave + lane;
+        if (j < total) {
+          float *d = spair + (j >> 1) * 4 + (j & 1);
+          d[0] = rec[u].x;
+          d[2] = rec[u].y;
+          d[kGZg] = rec[u].z;
+          d[kGZg + 2] = __int_as_float(gpos[u]);
+        }
+      }
+    }
+    wave_sync_mem();
+    NV_GT(ts1);
+    NV_GADD(4, ts0, ts1);
+#ifdef NAVGPU_STAMPS
+    gst[7] += 1;
+#endif
+    // ---- the round's queries, one per lane (k_knnw's scan, exact stage and
+    // certificate on the lane's block [t0, t1))
+    if (in && lane < lb) {
+      const int c[3] = {qx, qrow % g1, qrow / g1};
+      const int t0 = pre + (ga - A), t1 = pre + (gb - A);
+      const double qr[3] = {qv[0] - G.c[0], qv[1] - G.c[1], qv[2] - G.c[2]};
+      const double Dq = fmax(G.Dt, fmax(fabs(qr[0]), fmax(fabs(qr[1]), fabs(qr[2]))));
+      // each f32 difference is within dl of the exact one: the staged target
+      // offset and the query's carry <= u Dq each (u = 2^-24, plus the f64
+      // subtraction's 2^-53), the f32 subtraction <= 2 u Dq
+      const double dl = Dq * 0x1p-21;
+      const f2 qx2 = {(float)qr[0], (float)qr[0]}, qy2 = {(float)qr[1], (float)qr[1]},
+               qz2 = {(float)qr[2], (float)qr[2]};
+      const double Lr = block_reach(G, qv, c, 1);
+      uint32_t key[KL];
+#pragma unroll
+      for (int s = 0; s < KL; ++s) key[s] = kNoKey;
+      auto ins = [&](uint32_t kk) {  // keep the K+1 smallest keys sorted
+#pragma unroll
+        for (int s = K; s > 0; --s) key[s] = umed3(key[s - 1], key[s], kk);
+        key[0] = min(key[0], kk);
+      };
+      auto dist2 = [&](const float *p) {  // packed f32 squared distances of a pair
+        const float4 xy = *(const float4 *)p;
+        const float2 zz = *(const float2 *)(p + kGZg);
+        const f2 fx2 = f2{xy.x, xy.y} - qx2, fy2 = f2{xy.z, xy.w} - qy2,
+                 fz2 = f2{zz.x, zz.y} - qz2;
+        return __builtin_elementwise_fma(fz2, fz2, __builtin_elementwise_fma(fy2, fy2, fx2 * fx2));
+      };
+      const int ta = t0 & ~1;
+      const int npr = (t1 - ta + 1) >> 1;  // pairs the block touches
+      const bool overflow = (t1 - ta) > (1 << kKeyBits);
+      const float *cur = spair + (ta >> 1) * 4;
+      if (npr > 0) {  // first pair: may start before the block (odd t0) or end past it
+        const f2 d = dist2(cur);
+        const uint32_t k0 = knn_key(d[0], vmask, 0u), k1 = knn_key(d[1], vmask, 1u);
+        if (ta >= t0) ins(k0);
+        if (ta + 1 < t1) ins(k1);
+        cur += 4;
+      }
+      if (npr > 2) {  // interior pairs: the key's local id is the wave-uniform pair counter
+        const float *lastp = spair + ((ta >> 1) + npr - 1) * 4;
+        uint32_t v2 = 2;
+        float4 xy = *(const float4 *)cur;
+        float2 zz = *(const float2 *)(cur + kGZg);
+        do {
+          const float4 nxy = *(const float4 *)(cur + 4);
+          const float2 nzz = *(const float2 *)(cur + 4 + kGZg);
+          const f2 fx2 = f2{xy.x, xy.y} - qx2, fy2 = f2{xy.z, xy.w} - qy2,
+                   fz2 = f2{zz.x, zz.y} - qz2;
+          const f2 d =
+              __builtin_elementwise_fma(fz2, fz2, __builtin_elementwise_fma(fy2, fy2, fx2 * fx2));
+          ins(knn_key(d[0], vmask, v2));
+          ins(knn_key(d[1], vmask, v2 + 1));
+          cur += 4;
+          v2 += 2;
+          xy = nxy;
+          zz = nzz;
+        } while (cur < lastp);
+      }
+      if (npr > 1) {  // last pair: may end past the block
+        const f2 d = dist2(cur);
+        const uint32_t lid = (uint32_t)(2 * (npr - 1)) & kKeyMask;
+        const uint32_t k0 = (__float_as_uint(d[0]) & vmask) | lid;
+        const uint32_t k1 = (__float_as_uint(d[1]) & vmask) | (lid + 1);
+        ins(k0);
+        if (ta + 2 * (npr - 1) + 1 < t1) ins(k1);
+      }
+      NV_GT(ts2);
+      NV_GADD(5, ts1, ts2);
+      bool ok = !overflow && Dq < 1e17;
+      // exact f64 stage on the K best keys
+      double ed[K];
+      int ei[K];
+      if (key[0] != kNoKey) {
+        int gq[K];
+#pragma unroll
+        for (int s = 0; s < K; ++s) {
+          const uint32_t kk = key[s] != kNoKey ? key[s] : key[0];
+          const int p = min(max(ta + (int)(kk & kKeyMask), t0), max(t1 - 1, t0));
+          gq[s] = __float_as_int(spair[kGZg + (p >> 1) * 4 + 2 + (p & 1)]);
+        }
+        // all 2 K gathers in flight before any is used
+        double2 gxy[K], gzi[K];
+#pragma unroll
+        for (int s = 0; s < K; ++s) {
+          bad |= (unsigned)gq[s] >= (unsigned)ntg;
+          const PRec *tp = tsort + min(max(gq[s], 0), max(ntg - 1, 0));
+          gxy[s] = *(const double2 *)&tp->x;
+          gzi[s] = *(const double2 *)&tp->z;
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int s = 0; s < K; ++s) {
+          const bool val = key[s] != kNoKey;
+          const double2 xy = gxy[s], zi = gzi[s];
+          const double pz = zi.x;
+          const int pid = __double2loint(zi.y);
+          const double ddx = xy.x - qv[0], ddy = xy.y - qv[1], ddz = pz - qv[2];
+          const double dsq = ddx * ddx + ddy * ddy + ddz * ddz;  // utils/kdtree.c:16
+          ei[s] = val ? pid : -1;
+          ed[s] = val ? __builtin_sqrt(dsq) : INFINITY;
+          if (val && !(ed[s] < INFINITY)) {  // an inf/NaN distance is never a neighbour (kdtree.c:117)
+            ed[s] = INFINITY;
+            ei[s] = -1;
+            ok = false;
+          }
+        }
+      } else {
+#pragma unroll
+        for (int s = 0; s < K; ++s) {
+          ed[s] = INFINITY;
+          ei[s] = -1;
+        }
+      }
+      // certificate bound on every candidate left out
+      double B = INFINITY;
+      if (Lr < INFINITY) {
+        const double Lg = Lr - 2.0 * G.delta;
+        B = Lg > 0.0 ? Lg * Lg : 0.0;
+      }
+      if (key[K] != kNoKey) {
+        const double V = (double)__uint_as_float(key[K] & vmask);
+        B = fmin(B, V - f32_err(V, dl));
+      }
+      bool sorted = true;
+#pragma unroll
+      for (int s = 1; s < K; ++s) sorted &= !knn_less_bf(ed[s], ei[s], ed[s - 1], ei[s - 1]);
+      for (int pass = 0; pass < K - 1 && __any(!sorted); ++pass) {
+#pragma unroll
+        for (int u = 1; u < K; ++u) knn_cx(ed[u - 1], ei[u - 1], ed[u], ei[u]);
+        sorted = true;
+#pragma unroll
+        for (int s = 1; s < K; ++s) sorted &= !knn_less_bf(ed[s], ei[s], ed[s - 1], ei[s - 1]);
+      }
+      const double dk = ed[K - 1];
+      const double dk2 = dk * dk;
+      if (dk < INFINITY)
+        ok = ok && B > dk2 * (1.0 + 0x1p-46);
+      else
+        ok = ok && B == INFINITY;
+      if (ok) {
+        const size_t q = (size_t)qidx;
+        if (K % 4 == 0 && L_.vec_out) {
+#pragma unroll
+          for (int s = 0; s < K; s += 4)
+            *(int4 *)(oidx + q * K + s) = make_int4(ei[s], ei[s + 1], ei[s + 2], ei[s + 3]);
+#pragma unroll
+          for (int s = 0; s < K; s += 2)
+            *(double2 *)(odist + q * K + s) = make_double2(ed[s], ed[s + 1]);
+        } else {
+#pragma unroll
+          for (int s = 0; s < K; ++s) {
+            oidx[q * K + s] = ei[s];
+            odist[q * K + s] = ed[s];
+          }
+        }
+      } else {
+        push_slow(L_, qi, (dk < INFINITY && !overflow) ? dk2 * (1.0 + 0x1p-46) : INFINITY);
+      }
+      NV_GT(ts3);
+      NV_GADD(6, ts2, ts3);
+    }
+    la = lb;
+    wave_sync_mem();  // LDS is restaged by the next round
+  }
+  if (__any(bad) && lane == 0) atomicOr(L_.err, 1);
+#ifdef NAVGPU_STAMPS
+  gst[1] = __builtin_amdgcn_s_memrealtime();
+  gst[2] = __builtin_amdgcn_s_getreg((31 << 11) | 4);    // HW_REG_HW_ID
+  gst[3] = __builtin_amdgcn_s_getreg((31 << 11) | 20);   // HW_REG_XCC_ID
+  // the scan and exact-stage times: the wave's (the max over its lanes)
+#pragma unroll
+  for (int i = 5; i < 7; ++i) {
+    unsigned long long v = gst[i];
+    for (int o = 32; o > 0; o >>= 1) {
+      const unsigned long long w = (unsigned long long)__shfl_xor((long long)v, o, kWave);
+      v = v > w ? v : w;
+    }
+    gst[i] = v;
+  }
+  if (lane == 0 && chunk < kGStampChunks)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) g_gstamps[chunk][i] = gst[i];
+#endif
+}
+
 // ============================================================ k_knn_slow
 // insert (d, id) into the sorted exact list kd/ki if it ranks among the K
 template <int K>
@@ -2029,14 +2514,14 @@ __global__ __launch_bounds__(256) void k_knn_slow(const GridParams *__restrict__
   }
 }
 
-// counters of the last call: [n_unstaged, n_slow, pad, pad]
+// counters of the last call: [n_unstaged, n_slow, err, pad]
 long long read_counter(navgpu_ctx *ctx, int which) {
   if (!ctx) return -1;
   auto it = ctx->bufs.find(kStats);
   if (it == ctx->bufs.end() || !it->second.first) return -1;
-  int v[2] = {0, 0};
+  int v[4] = {0, 0, 0, 0};
   if (hipStreamSynchronize(ctx->stream) != hipSuccess) return -1;
-  if (hipMemcpy(v, it->second.first, 8, hipMemcpyDeviceToHost) != hipSuccess) return -1;
+  if (hipMemcpy(v, it->second.first, 16, hipMemcpyDeviceToHost) != hipSuccess) return -1;
   return (long long)v[which];
 }
 
@@ -2131,10 +2616,21 @@ static int knn_run(navgpu_ctx *ctx, const double *tgt, size_t nt, const double *
   RC(ws(ctx, kQSort, nq, &qcell));
   int *qraw;
   RC(ws(ctx, kQSlot, nq, &qraw));
+  const int mode = ctx->knn_mode;
+  // k_knng's row neighbourhood lists: 9 positions per target, and g0 + 1
+  // column starts per grid row (rows * (g0 + 1) <= 2 ncells <= 2 cap)
+  int *npg = nullptr, *gl = nullptr;
+  const long long ngl = std::max<long long>(9LL * (long long)nt, 1);
+  if (mode == 2) {
+    ARG_CHECK(ngl < INT32_MAX);
+    RC(ws(ctx, kNpg, 2 * (size_t)cap + 2, &npg));
+    RC(ws(ctx, kGl, (size_t)ngl, &gl));
+  }
+  J.sglobal = mode == 2;
   J.s[0].p = tgt;
   J.s[1].p = queries;
   J.s[0].start = tstart;
-  J.s[1].start = ctx->knn_mode == 1 ? nullptr : qstart;  // k_knnw reads no query starts
+  J.s[1].start = mode ? nullptr : qstart;  // k_knnw / k_knng read no query starts
   J.s[0].bin = tbin;
   J.s[1].bin = nullptr;
   J.s[0].key = nullptr;
@@ -2165,13 +2661,13 @@ static int knn_run(navgpu_ctx *ctx, const double *tgt, size_t nt, const double *
     A.n = nt;
     A.nq = nq;
     const dim3 gb(J.s[0].nblk + J.s[1].nblk);
-    hipLaunchKernelGGL(k_bin_hist, gb, dim3(256), 0, s, J, A, gp, counters, tab);
+    hipLaunchKernelGGL(k_bin_hist, gb, dim3(256), 4 * (size_t)J.nb, s, J, A, gp, counters, tab);
     CHECK_LAUNCH("k_bin_hist");
     const dim3 gc(2 * ((J.nb + kColB - 1) / kColB));
     hipLaunchKernelGGL(k_bin_colscan, gc, dim3(kColB * kColY), 0, s, tab, J.nb, J.s[0].tab,
                        J.s[0].nblk, J.s[1].tab, J.s[1].nblk, btot);
     CHECK_LAUNCH("k_bin_colscan");
-    hipLaunchKernelGGL(k_bin_scatter, gb, dim3(256), 0, s, J, gp, (const int *)tab,
+    hipLaunchKernelGGL(k_bin_scatter, gb, dim3(256), 4 * (size_t)J.nb, s, J, gp, (const int *)tab,
                        (const int *)btot, bbase);
     CHECK_LAUNCH("k_bin_scatter");
     // staged query placement when its LDS fits beside a 2^shift count table
@@ -2183,12 +2679,20 @@ static int knn_run(navgpu_ctx *ctx, const double *tgt, size_t nt, const double *
     hipLaunchKernelGGL(k_bin_fine, dim3(2 * J.nb), dim3(kBinFineThreads), lds, s, J, gp,
                        (const int *)bbase, nscan, st_q ? kFineStage : 0);
     CHECK_LAUNCH("k_bin_fine");
+    if (mode == 2) {
+      // tasks (64 columns of a row) <= 2 cap / 64 + rows; a few per wave
+      const unsigned nbl = std::min<unsigned>(1024, std::max<unsigned>(1, grid1d(2 * (size_t)cap, 64 * kNbWaves * 2)));
+      hipLaunchKernelGGL(k_nb_fill, dim3(nbl), dim3(kWave * kNbWaves), 0, s, gp,
+                         (const int *)tstart, npg, gl);
+      CHECK_LAUNCH("k_nb_fill");
+    }
   }
   KnnLists lists;
   RC(ws(ctx, kSlowQ, nq, &lists.slow_q));
   RC(ws(ctx, kSlowThr, nq, &lists.slow_thr));
   lists.n_unstaged = counters;
   lists.n_slow = counters + 1;
+  lists.err = counters + 2;
   lists.vec_out = ((uintptr_t)idx % 16 == 0 && (uintptr_t)dist % 16 == 0) ? 1 : 0;
   TimedRegion tr(ctx, "knn_query");
   // tiles are walked by a grid of 8 x nbx blocks (block b -> XCD b % 8, the
@@ -2204,11 +2708,15 @@ static int knn_run(navgpu_ctx *ctx, const double *tgt, size_t nt, const double *
   // dealt to the XCDs in contiguous ranges
   const int nchunk = (int)((nq + kWave - 1) / kWave);
   const dim3 gw(8 * (((nchunk + 7) / 8 + kWPB - 1) / kWPB)), bw(kWave * kWPB);
-  const bool waves = ctx->knn_mode == 1;
   const QSide QS{queries, qperm, qcell};
+  const dim3 gg(8 * (unsigned)((nchunk + 7) / 8));
 #define KNN_CASE(KK)                                                                        \
   case KK:                                                                                  \
-    if (waves)                                                                              \
+    if (mode == 2)                                                                          \
+      hipLaunchKernelGGL((k_knng<KK>), gg, dim3(kWave), 0, s, gp, (const int *)npg,         \
+                         (const int *)gl, (int)ngl, tsort, srec, QS, (int)nq, (int)nt, idx,  \
+                         dist, lists);                                                      \
+    else if (mode == 1)                                                                     \
       hipLaunchKernelGGL((k_knnw<KK>), gw, bw, 0, s, gp, tstart, tsort, srec, QS, (int)nq,      \
                          (int)nt, idx, dist, lists);                                        \
     else                                                                                    \
@@ -2264,7 +2772,7 @@ int navgpu_knn_host(navgpu_ctx *ctx, const double *tgt, size_t nt, const double 
   HIP_TRY(hipMemcpyAsync(idx, di, 4 * nq * k, hipMemcpyDeviceToHost, ctx->stream));
   HIP_TRY(hipMemcpyAsync(dist, dd, 8 * nq * k, hipMemcpyDeviceToHost, ctx->stream));
   HIP_TRY(hipStreamSynchronize(ctx->stream));
-  return NAVGPU_OK;
+  return navgpu_knn_check(ctx);
 }
 
 int navgpu_pair_knn_dev(navgpu_ctx *ctx, const double *src, const double *tgt, int R, int C,
@@ -2299,5 +2807,29 @@ int navgpu_pair_knn_dev(navgpu_ctx *ctx, const double *src, const double *tgt, i
 long long navgpu_knn_fallbacks(navgpu_ctx *ctx) { return read_counter(ctx, 1); }
 
 long long navgpu_knn_overflows(navgpu_ctx *ctx) { return read_counter(ctx, 0); }
+
+#ifdef NAVGPU_STAMPS
+// stamps builds only (not in navgpu.h): k_knng's per-chunk timeline of the
+// last call, 8 words per chunk, up to n chunks; returns the chunks copied
+int navgpu_debug_knng_timeline(unsigned long long *out, int n) {
+  n = std::min(n, kGStampChunks);
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_gstamps), (size_t)n * 64) != hipSuccess) return -1;
+  return n;
+}
+#endif
+
+int navgpu_knn_check(navgpu_ctx *ctx) {
+  ARG_CHECK(ctx);
+  const long long e = read_counter(ctx, 2);
+  if (e < 0) {
+    nv::set_err("knn_check: could not read the call's counters");
+    return NAVGPU_EHIP;
+  }
+  if (e) {
+    nv::set_err("knn: a kernel clamped an out-of-range index (internal error)");
+    return NAVGPU_EINTERNAL;
+  }
+  return NAVGPU_OK;
+}
 
 }  // extern "C"

@@ -2873,7 +2873,7 @@ int navgpu_create(int device, void *stream, navgpu_ctx **out) {
   c->device = device;
   if (const char *st = getenv("NAVGPU_KNN_STATS")) c->knn_stats = *st && *st != '0';
   if (const char *o = getenv("NAVGPU_KNN_BLOCKS")) c->knn_blocks = atoi(o);
-  if (const char *o = getenv("NAVGPU_KNN_MODE")) c->knn_mode = atoi(o) == 0 ? 0 : 1;
+  if (const char *o = getenv("NAVGPU_KNN_MODE")) c->knn_mode = std::min(std::max(atoi(o), 0), 2);
   if (const char *o = getenv("NAVGPU_KNN_SX")) {
     const int v = atoi(o);
     if (v >= 1 && v <= kKnnMaxSx) c->knn_sx = v;

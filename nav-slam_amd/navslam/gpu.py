@@ -83,6 +83,7 @@ def _declare(L):
         "navgpu_timing_count": (C.c_int, [_vp, C.c_char_p]),
         "navgpu_knn_fallbacks": (C.c_longlong, [_vp]),
         "navgpu_knn_overflows": (C.c_longlong, [_vp]),
+        "navgpu_knn_check": (C.c_int, [_vp]),
         "navgpu_rows_tie_rows": (C.c_longlong, [_vp]),
     }
     for name, (res, args) in sig.items():
@@ -185,6 +186,11 @@ class NavGpu:
         """k_knn tiles of the last knn call that overflowed the LDS tile and
         ran from global memory."""
         return self.L.navgpu_knn_overflows(self.h)
+
+    def knn_check(self):
+        """Raises NavGpuError (NAVGPU_EINTERNAL) when a k-NN kernel of the last
+        knn call met an out-of-range index (synchronises)."""
+        self._check(self.L.navgpu_knn_check(self.h), "knn_check")
 
     def rows_tie_rows(self):
         """Rows of the last rows_match call that had a distance tie and ran

@@ -504,6 +504,33 @@ def test_knn_vs_brute(gpu, orc, k):
         _eq(gd, rd, f"k={k} dist n={len(tgt)}")
 
 
+def test_knn_error_flag_stays_clear(gpu):
+    """Every k-NN kernel clamps the list, cloud and record indices it loads
+    through (so a logic error cannot fault the device) and flags the call
+    when a clamp changed one (navgpu_knn_check -> NAVGPU_EINTERNAL). The
+    small, degenerate and LDS-overflow inputs must leave it clear, through
+    the device entry point (navgpu_knn_host checks it itself)."""
+    import torch
+    rng = np.random.default_rng(7)
+    dev = torch.device("cuda", 0)
+    cases = [(rng.uniform(0, 1000, (5000, 3)), rng.uniform(-50, 1050, (3000, 3))),
+             (rng.uniform(0, 1, (7, 3)), rng.uniform(0, 1, (50, 3))),
+             (np.zeros((100, 3)), rng.uniform(-1, 1, (40, 3))),
+             (np.zeros((3000, 3)), np.zeros((300, 3))),          # one overfull cell
+             (np.c_[rng.uniform(0, 100, 3000), np.zeros(3000), np.zeros(3000)],
+              rng.uniform(0, 100, (500, 3))),
+             (np.zeros((0, 3)), rng.uniform(0, 1, (10, 3))),
+             (_clustered(rng, 20000, 6, 0.5, 1000.0), rng.uniform(0, 1000, (4000, 3)))]
+    for t, q in cases:
+        tt = torch.from_numpy(np.ascontiguousarray(t)).to(dev)
+        qq = torch.from_numpy(np.ascontiguousarray(q)).to(dev)
+        for k in (1, 8):
+            idx = torch.empty((len(q), k), dtype=torch.int32, device=dev)
+            dst = torch.empty((len(q), k), dtype=torch.float64, device=dev)
+            gpu.knn_dev(tt if len(t) else qq, len(t), qq, len(q), k, idx, dst)
+            gpu.knn_check()
+
+
 def _clustered(rng, n, centers, sigma, box):
     c = rng.uniform(0, box, (centers, 3))
     pts = c[rng.integers(0, centers, n)] + rng.normal(0, sigma, (n, 3))
