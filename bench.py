@@ -796,12 +796,12 @@ def main():
     return out
 
 
-QUERY_KERNELS = ("k_knnw<", "k_knn<", "k_knn_slow<")
-# the query pass launched once per step: k_knnw (r4 default) or k_knn
-# (NAVGPU_KNN_MODE=0)
-QUERY_MAIN = ("k_knnw<", "k_knn<")
+QUERY_KERNELS = ("k_knnw<", "k_knng<", "k_knn_slow<")
+# the query pass launched once per step: k_knnw (NAVGPU_KNN_MODE=1) or k_knng
+# (2: row neighbourhood lists, r5)
+QUERY_MAIN = ("k_knnw<", "k_knng<")
 BUILD_KERNELS = ("k_bbox_partial", "k_grid_params", "k_bin_hist", "k_bin_colscan",
-                 "k_bin_scatter", "k_bin_fine")
+                 "k_bin_scatter", "k_bin_fine", "k_nb_fill")
 # per-row workloads: the kernels of one step and the kernel launched once per
 # step (the per-step divisor)
 ROWS_KERNELS = ("k_curvature", "k_rows_screen", "k_rows_match")

@@ -19,18 +19,19 @@
 //                                   LDS atomics only: the targets as
 //                                   cell-sorted 32-B PRec records (f64 point,
 //                                   index, x column) and 16-B SRec staging
-//                                   records (f32 offset from the cell centre),
-//                                   the queries as a cell-sorted permutation
-//                                   and their cells
-//   k_knnw<K>                       (default) one wave per chunk of 64
+//                                   records (f32 offsets), the queries as
+//                                   cell-sorted 32-B records (point, index,
+//                                   cell)
+//   k_nb_fill                       (mode 2) the row neighbourhood lists
+//   k_knnw<K>                       (mode 1) one wave per chunk of 64
 //                                   cell-sorted queries: the chunk's row
 //                                   pieces staged in LDS column-major, one
 //                                   query per lane: packed-f32 keys into a
 //                                   sorted top-(K+1) (v_med3 insertion), f64
 //                                   exact stage, a certificate that the
 //                                   answer is exact
-//   k_knn<K>                        (NAVGPU_KNN_MODE=0) the r3 tile form of
-//                                   the same pass, kept for A/B
+//   k_knng<K>                       (mode 2) the same pass, each chunk's
+//                                   image staged as slices of the row lists
 //   k_knn_slow<K>                   the uncertified rest, one wave per query
 #include "navgpu_common.h"
 
@@ -51,7 +52,6 @@ struct GridParams {
   int ncells;
   int sx;                 // x cells per h: a query's block is cells x-sx .. x+sx,
                           // y-1 .. y+1, z-1 .. z+1 (the reach is >= h on every axis)
-  int tile_w;             // query cells (x) per k_knn tile
   int clamped;            // some axis hit the 2048-cell cap: its boundary cells
                           // hold points beyond their nominal box
   double c[3];            // (r5) the grid's centre: the one f32 frame of k_knng
@@ -71,51 +71,11 @@ struct __align__(16) SRec {
   int cx;
 };
 
-// ---- k_knn tile geometry (LDS budget: 4 blocks of 192 threads per CU)
-#ifndef NAVGPU_KNN_TILE_THREADS
-#define NAVGPU_KNN_TILE_THREADS 192
-#define NAVGPU_KNN_TILE_REC 1568
-#define NAVGPU_KNN_TILE_COLS 136
-#define NAVGPU_KNN_TILE_Q 150.0
-#endif
-constexpr int kTileThreads = NAVGPU_KNN_TILE_THREADS;  // 3 waves: a ~145-query tile fills them
-// waves per SIMD k_knn's registers must allow: 5 blocks of 3 waves per CU
-// (the LDS limit) need 4, i.e. <= 128 VGPRs
-#ifndef NAVGPU_KNN_MINW
-#define NAVGPU_KNN_MINW 4
-#endif
-constexpr int kKnnMinWaves = NAVGPU_KNN_MINW;
-constexpr int kTileRec = NAVGPU_KNN_TILE_REC;     // staged records per tile (16 B each)
-constexpr int kTilePairs = kTileRec / 2 + 2;  // two spare pairs: read-ahead
-constexpr int kZgOff = 4 * kTilePairs;        // floats from the XY plane to the ZG plane
-constexpr int kTileCols = NAVGPU_KNN_TILE_COLS;     // staged columns per tile + 1
-constexpr double kTileQueries = NAVGPU_KNN_TILE_Q;  // target queries per tile
-// survivor lists (NAVGPU_KNN_LIST=1): keys below a threshold are appended to
-// a per-lane LDS list and inserted into the sorted K+1 in batches; off by
-// default (the list's LDS costs a block per CU, r3 A/B in DESIGN.md §4)
-#ifndef NAVGPU_KNN_LIST
-#define NAVGPU_KNN_LIST 0
-#endif
-constexpr bool kList = NAVGPU_KNN_LIST;
-constexpr int kListCap = 12;       // survivors a lane holds before a drain
-#ifndef NAVGPU_KNN_PREFETCH
-#define NAVGPU_KNN_PREFETCH 1
-#endif
-constexpr bool kPrefetch = NAVGPU_KNN_PREFETCH;  // pipelined LDS reads in the scan
 constexpr int kKeyBits = 8;        // local id in the low bits of a packed key
 constexpr uint32_t kKeyMask = (1u << kKeyBits) - 1;
 constexpr uint32_t kNoKey = 0xffffffffu;
 
 constexpr int kBBoxBlocks = 256;  // bbox partials (every k_bin_hist block reduces them)
-
-// Timing-only ablations of k_knn (never in the product build: -DNAVGPU_ABL=...
-// in scripts/build_variants.sh); the results are wrong in such builds.
-#ifndef NAVGPU_ABL
-#define NAVGPU_ABL 0
-#endif
-constexpr int kAbl = NAVGPU_ABL;
-constexpr int kAblNoQuery = 1;  // staging and barriers only
-constexpr int kAblNoExact = 2;  // no f64 exact stage: keys decoded, one store per query
 
 // per-block min/max of the finite coordinates -> part[block][6]
 __global__ __launch_bounds__(256) void k_bbox_partial(const double *__restrict__ p,
@@ -176,7 +136,7 @@ __device__ void grid_params_block(const GridArgs A, GridParams *out) {
   const double *part = A.part;
   const int nparts = A.nparts, cap = A.cap, sx = A.sx;
   const double occ = A.occ;
-  const size_t n = A.n, nq = A.nq;
+  const size_t n = A.n;
   __shared__ double s[4][6];
   double v6[6] = {INFINITY, INFINITY, INFINITY, -INFINITY, -INFINITY, -INFINITY};
   for (int b = threadIdx.x; b < nparts; b += blockDim.x)
@@ -213,7 +173,6 @@ __device__ void grid_params_block(const GridArgs A, GridParams *out) {
     G.sx = 1;
     G.emax = 0.0;
     G.ncells = 1;
-    G.tile_w = 1;
     G.clamped = 0;
     for (int a = 0; a < 3; ++a) G.c[a] = 0.5;
     G.Dt = 1.0;
@@ -266,17 +225,6 @@ __device__ void grid_params_block(const GridArgs A, GridParams *out) {
     half = fmax(half, 0.5 * (g[a] * G.e[a]));
   }
   G.Dt = (clamped ? fmax(half, emax) : half) + 4.0 * G.delta;
-  // tile width: ~kTileQueries queries per tile, and its 9 staged row
-  // segments of W + 2 sx cells within ~90 % of the LDS record budget;
-  // balanced: the fewest tiles per grid row at that width, then equal widths
-  // (a ragged last tile would pay a full staging + barrier cycle for a few
-  // cells)
-  const double occ_q = (double)nq / G.ncells, occ_t = (double)n / G.ncells;
-  double w = fmin(kTileQueries / fmax(occ_q, 1e-9),
-                  0.9 * kTileRec / (9.0 * fmax(occ_t, 1e-9)) - 2.0 * sx);
-  const int wmax = (int)fmax(1.0, fmin((double)(kTileCols - 1 - 2 * sx), floor(w)));
-  const int tpr = (G.g[0] + wmax - 1) / wmax;
-  G.tile_w = (G.g[0] + tpr - 1) / tpr;
   *out = G;
 }
 
@@ -370,11 +318,11 @@ __global__ __launch_bounds__(kColB * kColY, kBuildMinW) void k_bin_colscan(int *
 //                (bucket, block) and moves to the coarse-bucketed array
 //                (BinPt, 32 B).
 //  k_bin_fine    one block per bucket: LDS counting sort over the bucket's
-//                2^shift cells, writes start[] for them; targets: every point
-//                at its final cell-sorted position as a PRec (k_knn stages
-//                row segments of them, coalesced); queries: only the
-//                permutation qperm[g] = the bucketed position (k_knn reads a
-//                tile's queries from one or two buckets: L2-local gathers).
+//                2^shift cells, writes start[] for them (targets); every
+//                point at its final cell-sorted position: targets as a PRec
+//                (the exact stage's f64 record) and an SRec (the f32 record
+//                the query passes stage), queries as their BinPt (the query
+//                passes read 64 consecutive ones per chunk).
 //                Order inside a cell is unspecified: the k-NN result does not
 //                depend on it (ties are resolved by (distance, index)).
 // Side 0 = targets, side 1 = queries; both go through the same launches
@@ -895,452 +843,6 @@ __device__ __forceinline__ void push_slow(const KnnLists &L_, int qi, double thr
   L_.slow_thr[e] = thr;
 }
 
-// ============================================================ k_knn
-// Global-mode exact k-NN over tiles of W consecutive x cells of one grid row.
-// Cells are h/sx wide in x and h in y, z, so a query's block (cells x-sx ..
-// x+sx, y-1 .. y+1, z-1 .. z+1) reaches >= h from it on every axis while
-// spanning only (2 sx + 1)/sx h in x.
-//
-// Staging. A tile stages the 9 neighbouring row segments (cells xa-sx ..
-// xb+sx) into LDS COLUMN-major: for each x cell j, the records of its 9
-// (y, z) rows follow one another, so a query's block is ONE contiguous slot
-// range [colst[i], colst[i + 2 sx + 1]). Each record is the f32 offset of the
-// f64 point from the tile's centre (x, y, z) and its cell-sorted position g,
-// in two pair-interleaved planes of 16 B per pair of records: XY (x0 x1 y0 y1)
-// and ZG (z0 z1 g0 g1). A tile whose segments exceed the LDS budget is cut
-// into narrower sub-ranges of query cells; a single cell whose block alone
-// exceeds it sends its queries to k_knn_slow.
-//
-// One query per lane (cell-sorted queries, read coalesced). The block is
-// walked in pairs of records from its even-aligned first slot ta: packed f32
-// squared distances (3 packed sub, 1 mul, 2 fma per pair), keys packed with
-// the wave-uniform pair offset as local id. By default every key goes
-// straight into the lane's sorted K+1 smallest (a branch-free median-of-3
-// network). With NAVGPU_KNN_LIST=1 (off: its LDS costs a resident block per
-// CU) a key is first appended to a per-lane LDS list if it is below the
-// lane's threshold T (at first the f32 image of R^2, R the radius holding
-// ~lambda targets at the block's density; after each drain, the (K+1)-th
-// key), and drains insert the listed keys in batches.
-//
-// Exact stage and certificate. The K best keys are re-evaluated with the
-// reference f64 formula from the cell-sorted f64 copy and ordered by
-// (distance, index). Every candidate left out is bounded below: outside the
-// block by the block's reach, (list variant only) rejected against the first
-// threshold by R^2, rejected or evicted by the (K+1)-th key V minus the f32
-// error. If
-// that bound exceeds the K-th exact dsq (times 1 + 2^-46), the answer is
-// exact; otherwise the query goes to k_knn_slow with the K-th dsq as bound.
-template <int K>
-__global__ __launch_bounds__(kTileThreads, kKnnMinWaves) void k_knn(
-    const GridParams *__restrict__ gp, const int *__restrict__ tstart,
-    const PRec *__restrict__ tsort, const int *__restrict__ qstart,
-    const QSide QS, int32_t *__restrict__ oidx,
-    double *__restrict__ odist, KnnLists L_, float lambda) {
-  __shared__ __attribute__((aligned(16))) float spair[2 * kZgOff];
-  // cbr[r][j]: the LDS slot of the record at cell-sorted position g of cell
-  // (row r, tile column j) is cbr[r][j] + g - sbase. Before that: the row
-  // segments' global starts (soff)
-  __shared__ int cbr[9][kTileCols];
-  __shared__ int colst[kTileCols];  // first slot of tile column j (whole tile)
-  __shared__ uint32_t slist[kList ? kListCap * kTileThreads : 1];
-  __shared__ int seg[9][2];  // each row segment's global [first, end)
-  __shared__ int scratch[kTileThreads / kWave + 1];
-  constexpr int KL = K + 1;
-  static_assert(K >= 1 && K <= 16, "K");
-  const GridParams G = *gp;
-  const int W = G.tile_w, S = G.sx;
-  const int tpr = (G.g[0] + W - 1) / W;
-  const int ntiles = tpr * G.g[1] * G.g[2];  // < cells < 2^31
-  // tiles dealt to the 8 XCDs in contiguous ranges (block b runs on XCD
-  // b % 8 under the observed round-robin placement; another placement only
-  // costs L2 hits), so each XCD's L2 holds only its slab of the cloud
-  const int xcd = blockIdx.x & 7;
-  const int t_hi = (int)((long long)ntiles * (xcd + 1) / 8);
-  const int tid = (int)threadIdx.x;
-  const int lane = tid & (kWave - 1), wv = tid / kWave;
-  const uint32_t vmask = ~kKeyMask;
-  NV_ACC_DECL;
-  // volume of a query's block, in units of h^3
-  const float vol_h3 = 9.0f * (float)(2 * S + 1) / (float)S;
-  for (int tile = (int)((long long)ntiles * xcd / 8) + (int)(blockIdx.x >> 3); tile < t_hi;
-       tile += (int)(gridDim.x >> 3)) {
-    NV_STAMP(tb0);
-    const int row = tile / tpr, chunk = tile - row * tpr;
-    const int y = row % G.g[1], z = row / G.g[1];
-    const int xa = chunk * W, xb = min(xa + W, G.g[0]) - 1;
-    const int ncol = xb - xa + 1 + 2 * S;  // tile columns j: cells xa - S + j
-    // tile centre: the f32 records are offsets from it
-    const double ot[3] = {G.o[0] + (xa + 0.5 * (xb - xa + 1)) * G.e[0],
-                          G.o[1] + (y + 0.5) * G.h, G.o[2] + (z + 0.5) * G.h};
-    // largest staged offset magnitude (cell-assignment slack included)
-    // (a clamped grid's boundary cells may hold anything inside the bbox)
-    const double Dt = G.clamped ? G.emax + 2.0 * G.h
-                                : fmax((0.5 * (xb - xa + 1) + S + 1) * G.e[0], 2.0 * G.h) +
-                                      4.0 * G.delta;
-    // ---- the 9 row segments' starts: soff[r][j] for j = 0 .. ncol (the
-    // row's end for cells past the grid)
-    if (tid <= ncol) {
-      int v[9];
-#pragma unroll
-      for (int r = 0; r < 9; ++r) {
-        const int yy = y + (r % 3) - 1, zz = z + (r / 3) - 1;
-        v[r] = 0;
-        if (yy >= 0 && yy < G.g[1] && zz >= 0 && zz < G.g[2]) {
-          const int x = min(max(xa - S + tid, 0), G.g[0]);  // x = g0: the row's end
-          v[r] = tstart[(zz * G.g[1] + yy) * G.g[0] + x];
-        }
-      }
-#pragma unroll
-      for (int r = 0; r < 9; ++r) cbr[r][tid] = v[r];
-    }
-    __syncthreads();
-    // ---- column counts, their exclusive scan (colst), and cbr in place
-    {
-      const int j = tid;
-      int sv[9], n[9], cs = 0;
-#pragma unroll
-      for (int r = 0; r < 9; ++r) {
-        sv[r] = j < ncol ? cbr[r][j] : 0;
-        n[r] = j < ncol ? cbr[r][j + 1] - sv[r] : 0;
-        cs += n[r];
-      }
-      if (j < 9) {
-        seg[j][0] = cbr[j][0];
-        seg[j][1] = cbr[j][ncol];
-      }
-      int total;
-      const int cex = block_excl_scan(cs, scratch, &total);  // barriers: cbr reads done
-      if (j <= ncol) colst[j] = cex;  // colst[ncol] = the total
-      if (j < ncol) {
-        int a = cex;
-#pragma unroll
-        for (int r = 0; r < 9; ++r) {
-          cbr[r][j] = a - sv[r];
-          a += n[r];
-        }
-      }
-    }
-    __syncthreads();
-    const int cell0 = (z * G.g[1] + y) * G.g[0] + xa - S;  // cell of tile column 0
-    // ---- sub-ranges of query columns [qa, qb] (tile columns S .. ncol-1-S)
-    // whose staged columns [qa - S, qb + S] fit the LDS budget; one
-    // sub-range unless the tile is unusually dense
-    for (int qa = S; qa <= ncol - 1 - S;) {
-      const int base0 = colst[qa - S];
-      const bool fits = tid >= qa && tid <= ncol - 1 - S && colst[tid + S + 1] - base0 <= kTileRec;
-      const int qb = qa - 1 + __syncthreads_count(fits);  // fits is a prefix of [qa, ..]
-      if (qb < qa) {
-        // one query cell whose block alone exceeds the budget: its queries
-        // go to k_knn_slow from an infinite bound
-        const int q0 = qstart[cell0 + qa], q1 = qstart[cell0 + qa + 1];
-        for (int qi = q0 + tid; qi < q1; qi += kTileThreads) {
-          push_slow(L_, qi, INFINITY);
-          atomicAdd(L_.n_unstaged, 1);
-        }
-        ++qa;
-        continue;
-      }
-      const int ja = qa - S, jb = qb + S;
-      const int sbase = colst[ja];
-      // ---- copy: each wave takes whole row segments (r = wave, wave + 3,
-      // wave + 6), so a record's row is wave-uniform; all loads of a batch
-      // are issued before any LDS write. Records outside [ja, jb] (a cut
-      // tile) are skipped.
-      constexpr int U = 2;
-      for (int r = wv; r < 9; r += kTileThreads / kWave) {
-        const int g0 = seg[r][0], nr = seg[r][1] - g0;
-        const int *cb = &cbr[r][0];
-        for (int k0 = 0; k0 < nr; k0 += U * kWave) {
-          PRec v[U];
-#pragma unroll
-          for (int u = 0; u < U; ++u) {
-            const int k = k0 + u * kWave + lane;
-            if (k < nr) v[u] = tsort[g0 + k];
-          }
-#pragma unroll
-          for (int u = 0; u < U; ++u) {
-            const int k = k0 + u * kWave + lane;
-            // the record's tile column (its cell lies in xa-S .. xb+S)
-            const int jj = v[u].cx - (xa - S);
-            if (k < nr && jj >= ja && jj <= jb) {
-              const int g = g0 + k;
-              const int slot = cb[jj] + g - sbase;
-              float *d = spair + (slot >> 1) * 4 + (slot & 1);
-              d[0] = (float)(v[u].x - ot[0]);
-              d[2] = (float)(v[u].y - ot[1]);
-              d[kZgOff] = (float)(v[u].z - ot[2]);
-              d[kZgOff + 2] = __int_as_float(g);
-            }
-          }
-        }
-      }
-      __syncthreads();
-      NV_STAMP(tb1);
-      NV_ACC(1, tb0, tb1);
-      // ---- the sub-range's queries
-      const int q0 = qstart[cell0 + qa], q1 = qstart[cell0 + qb + 1];
-      for (int qi = q0 + tid; qi < q1 && !(kAbl & kAblNoQuery); qi += kTileThreads) {
-        NV_STAMP(ts0);
-        const BinPt Q = qload(QS, qi);
-        const double qv[3] = {Q.x, Q.y, Q.z};
-        const int qcx = Q.cell - (z * G.g[1] + y) * G.g[0];  // the cell's x index
-        const int c[3] = {qcx, y, z};
-        const int i = qcx - (xa - S);  // tile column of the query's cell
-        const int t0 = colst[i - S] - sbase, t1 = colst[i + S + 1] - sbase;
-        const double qr[3] = {qv[0] - ot[0], qv[1] - ot[1], qv[2] - ot[2]};
-        const double Dq = fmax(Dt, fmax(fabs(qr[0]), fmax(fabs(qr[1]), fabs(qr[2]))));
-        const double dl = Dq * 0x1p-22;
-        const f2 qx2 = {(float)qr[0], (float)qr[0]}, qy2 = {(float)qr[1], (float)qr[1]},
-                 qz2 = {(float)qr[2], (float)qr[2]};
-        // first threshold: R^2 with R holding ~lambda targets at the block's
-        // density (R^3 = 3 lambda vol / (4 pi count))
-        // (none when the block reaches every face of the grid: then it holds
-        // every target and nothing needs filtering)
-        const int count = t1 - t0;
-        const double Lr = block_reach(G, qv, c, 1);
-        double Tgeo = INFINITY;
-        if (kList && count > 0 && Lr < INFINITY) {
-          const float r3 = 0.2387324146f * lambda * vol_h3 / (float)count;  // 3/(4 pi)
-          Tgeo = (double)__builtin_amdgcn_exp2f(__builtin_amdgcn_logf(r3) * (2.0f / 3.0f)) *
-                 (G.h * G.h);
-        }
-        const float Tf = f32_bound(Tgeo, dl);
-        uint32_t T = Tf < INFINITY ? (__float_as_uint(Tf) | kKeyMask) + 1u : kNoKey;
-        uint32_t key[KL];
-#pragma unroll
-        for (int s = 0; s < KL; ++s) key[s] = kNoKey;
-        auto ins = [&](uint32_t kk) {  // keep the K+1 smallest keys sorted
-#pragma unroll
-          for (int s = K; s > 0; --s) key[s] = umed3(key[s - 1], key[s], kk);
-          key[0] = min(key[0], kk);
-        };
-        // the lane's survivor list: entry e at slist[e * kTileThreads + tid];
-        // lo = the next free entry's offset
-        uint32_t *const lst = slist + tid;
-        int lo = 0;
-        auto drain = [&]() {
-          if constexpr (!kList) return;
-          const int cnt = lo / kTileThreads;
-          NV_STAMP(td0);
-          if (__any(cnt > 0)) {
-            int e = 0;
-            do {
-              NV_ACC(9, 0ull, 1ull);
-              const uint32_t v = lst[e * kTileThreads];  // stale past cnt: masked below
-              ins(e < cnt ? v : kNoKey);
-              ++e;
-            } while (__any(e < cnt));
-          }
-          lo = 0;
-          T = min(T, key[K]);
-          NV_STAMP(td1);
-          NV_ACC(10, td0, td1);
-        };
-        // branch-free append: the key is always written at the free entry
-        // and the entry kept only if it passes (no exec-mask juggling in the
-        // scan loop); a drain keeps lo <= (kListCap - 2) entries before a pair
-        auto offer = [&](uint32_t kk) {
-          if constexpr (kList) {
-            lst[lo] = kk;
-            lo += kk < T ? kTileThreads : 0;
-          } else {
-            ins(kk);
-          }
-        };
-        auto nearly_full = [&]() { return kList && lo > (kListCap - 2) * kTileThreads; };
-        auto dist2 = [&](const float *p) {  // packed f32 squared distances of a pair
-          const float4 xy = *(const float4 *)p;
-          const float2 zz = *(const float2 *)(p + kZgOff);
-          const f2 fx2 = f2{xy.x, xy.y} - qx2, fy2 = f2{xy.z, xy.w} - qy2,
-                   fz2 = f2{zz.x, zz.y} - qz2;
-          return __builtin_elementwise_fma(fz2, fz2,
-                                           __builtin_elementwise_fma(fy2, fy2, fx2 * fx2));
-        };
-        NV_STAMP(ts1);
-        const int ta = t0 & ~1;
-        const int np = (t1 - ta + 1) >> 1;  // pairs the block touches
-        const bool overflow = (t1 - ta) > (1 << kKeyBits);
-        const float *cur = spair + (ta >> 1) * 4;
-        if (np > 0) {  // first pair: may start before the block (odd t0) or end past it
-          const f2 d = dist2(cur);
-          const uint32_t k0 = knn_key(d[0], vmask, 0u), k1 = knn_key(d[1], vmask, 1u);
-          if (ta >= t0) offer(k0);
-          if (ta + 1 < t1) offer(k1);
-          cur += 4;
-        }
-        // interior pairs: both records inside the block; the key's local id
-        // is the wave-uniform pair counter. A lane leaves at its last pair.
-        if (np > 2) {
-          const float *last = spair + ((ta >> 1) + np - 1) * 4;
-          uint32_t v2 = 2;
-          if constexpr (kPrefetch) {
-            // software-pipelined: the next pair's LDS reads are issued before
-            // this pair's arithmetic (the read past the block's last interior
-            // pair lands on its last pair or a spare one)
-            float4 xy = *(const float4 *)cur;
-            float2 zz = *(const float2 *)(cur + kZgOff);
-            do {
-              const float4 nxy = *(const float4 *)(cur + 4);
-              const float2 nzz = *(const float2 *)(cur + 4 + kZgOff);
-              const f2 fx2 = f2{xy.x, xy.y} - qx2, fy2 = f2{xy.z, xy.w} - qy2,
-                       fz2 = f2{zz.x, zz.y} - qz2;
-              const f2 d = __builtin_elementwise_fma(
-                  fz2, fz2, __builtin_elementwise_fma(fy2, fy2, fx2 * fx2));
-              offer(knn_key(d[0], vmask, v2));
-              offer(knn_key(d[1], vmask, v2 + 1));
-              cur += 4;
-              v2 += 2;
-              xy = nxy;
-              zz = nzz;
-              if (__any(nearly_full())) drain();
-            } while (cur < last);
-          } else {
-            do {
-              const f2 d = dist2(cur);
-              offer(knn_key(d[0], vmask, v2));
-              offer(knn_key(d[1], vmask, v2 + 1));
-              cur += 4;
-              v2 += 2;
-              if (__any(nearly_full())) drain();
-            } while (cur < last);
-          }
-        }
-        if (np > 1) {  // last pair: may end past the block
-          const f2 d = dist2(cur);
-          const uint32_t lid = (uint32_t)(2 * (np - 1)) & kKeyMask;
-          // lid depends on the lane's np here: the plain and + or
-          const uint32_t k0 = (__float_as_uint(d[0]) & vmask) | lid;
-          const uint32_t k1 = (__float_as_uint(d[1]) & vmask) | (lid + 1);
-          if (__any(nearly_full())) drain();
-          offer(k0);
-          if (ta + 2 * (np - 1) + 1 < t1) offer(k1);
-        }
-        drain();
-        NV_STAMP(ts2);
-        bool ok = !overflow && Dq < 1e17;
-        if (kAbl & kAblNoExact) {  // timing-only: keep the keys live, one store
-          uint32_t acc = 0;
-#pragma unroll
-          for (int s = 0; s < KL; ++s) acc ^= key[s];
-          oidx[(size_t)Q.idx * K] = (int)acc + (int)ok;
-          continue;
-        }
-        // ---- exact f64 stage on the K best keys (none if the block was
-        // empty: then no slot is staged). All loads are issued unconditionally
-        // (an empty slot re-reads slot 0) so their latencies overlap;
-        // coordinates from the cell-sorted copy (L2-local).
-        double ed[K];
-        int ei[K];
-        if (key[0] != kNoKey) {
-          int gpos[K];
-#pragma unroll
-          for (int s = 0; s < K; ++s) {
-            const uint32_t kk = key[s] != kNoKey ? key[s] : key[0];
-            // clamped into the block so a corrupt id can never leave the tile
-            const int p = min(max(ta + (int)(kk & kKeyMask), t0), max(t1 - 1, t0));
-            gpos[s] = __float_as_int(spair[kZgOff + (p >> 1) * 4 + 2 + (p & 1)]);
-          }
-#pragma unroll
-          for (int s = 0; s < K; ++s) {
-            const bool val = key[s] != kNoKey;
-            // the 32-B record as two 16-B loads: (x, y) and (z, idx | cx)
-            const PRec *tp = tsort + gpos[s];
-            const double2 xy = *(const double2 *)&tp->x;
-            const double2 zi = *(const double2 *)&tp->z;
-            const double pz = zi.x;
-            const int pid = __double2loint(zi.y);
-            const double ddx = xy.x - qv[0], ddy = xy.y - qv[1], ddz = pz - qv[2];
-            const double dsq = ddx * ddx + ddy * ddy + ddz * ddz;  // utils/kdtree.c:16
-            ei[s] = val ? pid : -1;
-            ed[s] = val ? __builtin_sqrt(dsq) : INFINITY;
-            // an inf/NaN distance is never a neighbour (kdtree.c:117)
-            if (val && !(ed[s] < INFINITY)) {
-              ed[s] = INFINITY;
-              ei[s] = -1;
-              ok = false;
-            }
-          }
-        } else {
-#pragma unroll
-          for (int s = 0; s < K; ++s) {
-            ed[s] = INFINITY;
-            ei[s] = -1;
-          }
-        }
-        // ---- certificate bound on every candidate left out
-        double B = INFINITY;
-        if (Lr < INFINITY) {
-          const double Lg = Lr - 2.0 * G.delta;
-          B = Lg > 0.0 ? Lg * Lg : 0.0;
-        }
-        B = fmin(B, Tgeo);  // rejected against the first threshold: exact dsq > Tgeo
-        if (key[K] != kNoKey) {
-          const double V = (double)__uint_as_float(key[K] & vmask);
-          B = fmin(B, V - f32_err(V, dl));
-        }
-        // order by (distance, index): the truncated-key order is almost always
-        // right and a misordered survivor sits next to its place; bubble
-        // passes (branch-free compare-exchange) run until no lane of the wave
-        // is out of order, usually none
-        bool sorted = true;
-#pragma unroll
-        for (int s = 1; s < K; ++s) sorted &= !knn_less_bf(ed[s], ei[s], ed[s - 1], ei[s - 1]);
-        for (int pass = 0; pass < K - 1 && __any(!sorted); ++pass) {
-#pragma unroll
-          for (int u = 1; u < K; ++u) knn_cx(ed[u - 1], ei[u - 1], ed[u], ei[u]);
-          sorted = true;
-#pragma unroll
-          for (int s = 1; s < K; ++s) sorted &= !knn_less_bf(ed[s], ei[s], ed[s - 1], ei[s - 1]);
-        }
-        const double dk = ed[K - 1];
-        const double dk2 = dk * dk;  // >= the exact K-th dsq (sqrt rounds to nearest)
-        if (dk < INFINITY)
-          ok = ok && B > dk2 * (1.0 + 0x1p-46);
-        else
-          ok = ok && B == INFINITY;  // fewer than K neighbours: only if all was seen
-        if (ok) {
-          const size_t q = (size_t)Q.idx;
-          // a query's K results are contiguous: 16-B stores when K allows and
-          // the host found both outputs 16-B aligned (L_.vec_out)
-          if (K % 4 == 0 && L_.vec_out) {
-#pragma unroll
-            for (int s = 0; s < K; s += 4)
-              *(int4 *)(oidx + q * K + s) = make_int4(ei[s], ei[s + 1], ei[s + 2], ei[s + 3]);
-#pragma unroll
-            for (int s = 0; s < K; s += 2)
-              *(double2 *)(odist + q * K + s) = make_double2(ed[s], ed[s + 1]);
-          } else {
-#pragma unroll
-            for (int s = 0; s < K; ++s) {
-              oidx[q * K + s] = ei[s];
-              odist[q * K + s] = ed[s];
-            }
-          }
-        } else {
-          // K listed points have dsq <= dk2: a valid starting bound for the
-          // slow path. Not after an overfull block: its keys' offsets
-          // wrapped, so two slots can decode to the same record and the list
-          // may hold fewer than K distinct points.
-          push_slow(L_, qi, (dk < INFINITY && !overflow) ? dk2 * (1.0 + 0x1p-46) : INFINITY);
-        }
-        NV_STAMP(ts3);
-        NV_ACC(8, ts0, ts1);
-        NV_ACC(3, ts1, ts2);
-        NV_ACC(4, ts2, ts3);
-        NV_ACC(5, 0ull, 1ull);
-      }
-      NV_STAMP(tb2);
-      __syncthreads();  // LDS is restaged by the next sub-range or tile
-      NV_STAMP(tb3);
-      NV_ACC(2, tb1, tb2);
-      NV_ACC(7, tb2, tb3);
-      NV_ACC(6, 0ull, 1ull);
-      qa = qb + 1;
-    }
-  }
-  NV_ACC_FLUSH;
-}
-
 // ============================================================ k_knnw
 // The query pass in wave chunks (r4): one WAVE per chunk of 64 consecutive
 // cell-sorted queries, no block barriers. k_knn's tiles were W query cells of
@@ -1450,19 +952,13 @@ __global__ __launch_bounds__(kWave * kWPB, NAVGPU_KNNW_MINW) void k_knnw(const G
   const int qi = chunk * kWave + lane;
   const bool live = lane < nlive;
   BinPt Q;
-#ifdef NAVGPU_KNNW_CHECK
-  if (live && (QS.idx[qi] < 0 || QS.idx[qi] >= nq || QS.cell[qi] < 0)) {
-    printf("knnw chunk %d lane %d: query %d idx %d cell %d\n", chunk, lane, qi, QS.idx[qi],
-           QS.cell[qi]);
-    return;
-  }
-#endif
   Q = qload(QS, min(qi, nq - 1));  // (unconditional: see the table loads)
   // the query's cell: x, row = (z g1 + y); rows ascend over the lanes
   const int qrow = live ? Q.cell / g0 : 0x7fffffff;
   const int qx = live ? Q.cell - qrow * g0 : 0;
   const int qy = live ? qrow % g1 : 0, qz = live ? qrow / g1 : 0;
   const uint32_t vmask = ~kKeyMask;
+  int bad = 0;  // an index that had to be clamped (a logic error)
   // rows ascend over the live lanes: a lane starts (ends) a grid row when the
   // lane before (after) it holds another one (the shuffles run on every lane:
   // a lane masked off by a short-circuit would hand its neighbour garbage)
@@ -1622,10 +1118,6 @@ __global__ __launch_bounds__(kWave * kWPB, NAVGPU_KNNW_MINW) void k_knnw(const G
       }
     }
     wave_sync_mem();
-#ifdef NAVGPU_KNNW_CHECK
-    for (int q = lane; q < kWRec; q += kWave) spair[kWZg + (q >> 1) * 4 + 2 + (q & 1)] = __int_as_float(-1);
-    wave_sync_mem();
-#endif
     // ---- staging: per segment, its 9 row pieces as SRec (16 B: f32 offset
     // from the record's cell centre + x cell); every load of a segment in
     // flight before any is used; slot from cbr, x shift from dxc (the
@@ -1655,19 +1147,15 @@ __global__ __launch_bounds__(kWave * kWPB, NAVGPU_KNNW_MINW) void k_knnw(const G
           // every load is issued, unconditionally, from a position clamped
           // into the cloud (a per-element condition makes hipcc branch around
           // each load and wait for it: nine serial round trips); lanes past a
-          // row piece discard theirs below. (The clamp also keeps a logic
-          // error from reading past the cloud, which would fault the device.)
+          // row piece discard theirs below. A clamp inside a piece would be a
+          // logic error: it sets the call's error flag (navgpu_knn_check).
 #pragma unroll
           for (int r = 0; r < 9; ++r)
 #pragma unroll
             for (int u = 0; u < U; ++u) {
               const int k = k0 + u * kWave + lane;
-#ifdef NAVGPU_KNNW_CHECK
-              if (k < nr[r] && (glo[r] + k < 0 || glo[r] + k >= ntg))
-                printf("knnw chunk %d lane %d seg %d row %d: srec %d of %d (glo %d nr %d)\n",
-                       chunk, lane, si, r, glo[r] + k, ntg, glo[r], nr[r]);
-#endif
               // (a wave-uniform row base and a 32-bit lane offset)
+              bad |= (k < nr[r]) & ((unsigned)(glo[r] + k) >= (unsigned)ntg);
               v[r][u] = (srec + glo[r])[min(k, tlast - glo[r])];
             }
 #pragma unroll
@@ -1712,31 +1200,6 @@ __global__ __launch_bounds__(kWave * kWPB, NAVGPU_KNNW_MINW) void k_knnw(const G
     NV_ACC(3, r1, r2);
     // the last query cell of the lane's segment in the column-fit round (its frame)
     const int xl = __shfl(qx, min(sl, lbc - 1), kWave);
-#ifdef NAVGPU_KNNW_CHECK
-    if (in && lane < lb) {
-      const int t0 = colst[vcq - S], t1 = colst[vcq + S + 1];
-      int bad = -1;
-      for (int q = t0; q < t1; ++q)
-        if (__float_as_int(spair[kWZg + (q >> 1) * 4 + 2 + (q & 1)]) < 0) bad = q;
-      if (bad >= 0) {
-        printf("CHK chunk %d lane %d la %d lb %d lbc %d NC %d total %d vcq %d sf %d sl %d t0 %d t1 %d bad %d fb %llx qx %d qrow %d\n",
-               chunk, lane, la, lb, lbc, NC, total, vcq, sf, sl, t0, t1, bad, fb, qx, qrow);
-        for (int v = vcq - S; v <= vcq + S + 1; ++v) printf("CHK chunk %d colst[%d] = %d\n", chunk, v, colst[v]);
-      }
-    }
-    {
-      int si2 = 0;
-      for (unsigned long long b = fb; b; b &= b - 1, ++si2) {
-        const int f = (int)__builtin_ctzll(b);
-        const int lsl = min(rdlane(sl, f), lb - 1);
-        if (lane == 0 && (chunk == 5 || chunk == 36 || chunk == 40))
-          printf("SEG chunk %d si %d f %d lsl %d vc0 %d vlast %d x %d..%d row %d | %d %d %d %d %d %d %d %d %d / %d %d %d %d %d %d %d %d %d\n",
-                 chunk, si2, f, lsl, rdlane(pre, f), rdlane(cum, lsl) - 1, rdlane(qx, f), rdlane(qx, lsl), rdlane(qrow, f),
-                 sbnd[si2][0][0], sbnd[si2][1][0], sbnd[si2][2][0], sbnd[si2][3][0], sbnd[si2][4][0], sbnd[si2][5][0], sbnd[si2][6][0], sbnd[si2][7][0], sbnd[si2][8][0],
-                 sbnd[si2][0][1], sbnd[si2][1][1], sbnd[si2][2][1], sbnd[si2][3][1], sbnd[si2][4][1], sbnd[si2][5][1], sbnd[si2][6][1], sbnd[si2][7][1], sbnd[si2][8][1]);
-      }
-    }
-#endif
     // ---- the round's queries, one per lane (k_knn's scan, exact stage and
     // certificate on the lane's block [t0, t1))
     if (in && lane < lb) {
@@ -1827,12 +1290,8 @@ __global__ __launch_bounds__(kWave * kWPB, NAVGPU_KNNW_MINW) void k_knnw(const G
         double2 gxy[K], gzi[K];
 #pragma unroll
         for (int s = 0; s < K; ++s) {
-#ifdef NAVGPU_KNNW_CHECK
-          if (gpos[s] < 0 || gpos[s] >= ntg)
-            printf("knnw chunk %d lane %d: gpos %d of %d (key %x t0 %d t1 %d)\n", chunk, lane,
-                   gpos[s], ntg, key[s], t0, t1);
-#endif
-          gpos[s] = min(max(gpos[s], 0), max(ntg - 1, 0));  // (as the staging clamp above)
+          bad |= (unsigned)gpos[s] >= (unsigned)ntg;  // (flagged, as the staging clamp above)
+          gpos[s] = min(max(gpos[s], 0), max(ntg - 1, 0));
           const PRec *tp = tsort + gpos[s];
           gxy[s] = *(const double2 *)&tp->x;
           gzi[s] = *(const double2 *)&tp->z;
@@ -1914,6 +1373,7 @@ __global__ __launch_bounds__(kWave * kWPB, NAVGPU_KNNW_MINW) void k_knnw(const G
     la = lb;
     wave_sync_mem();  // LDS is restaged by the next round
   }
+  if (__any(bad) && lane == 0) atomicOr(L_.err, 1);
   NV_STAMP(w9);
   NV_ACC(8, w0, w9);
   NV_WFLUSH(chunk);
@@ -1969,6 +1429,15 @@ struct F3 {
   float x, y, z;
 };
 
+// Timing-only ablations (-DNAVGPU_ABL=bits, scripts/build_variants.sh; never
+// the product build, the results are wrong): 1 the exact stage's record
+// gathers, 8 the staged records read from a 1024-record window (L2-resident,
+// same request count); 4 no result stores.
+#ifndef NAVGPU_ABL
+#define NAVGPU_ABL 0
+#endif
+constexpr int kAbl = NAVGPU_ABL;
+
 template <int K>
 __global__ __launch_bounds__(kWave, NAVGPU_KNNG_MINW) void k_knng(
     const GridParams *__restrict__ gp, const int *__restrict__ npg, const int *__restrict__ gl,
@@ -1981,36 +1450,53 @@ __global__ __launch_bounds__(kWave, NAVGPU_KNNG_MINW) void k_knng(
   static_assert(K >= 1 && K <= 16, "K");
   const GridParams G = *gp;
   const int S = G.sx, g0 = G.g[0], g1 = G.g[1];
-  // chunks dealt to the 8 XCDs in contiguous ranges (block b -> XCD b % 8)
+  // chunks dealt to the 8 XCDs in contiguous pools (block b -> XCD b % 8):
+  // one chunk per wave, the pool's chunk b / 8. (Persistent waves were
+  // measured in r5 and lost, with the next chunk's cells and block bounds
+  // loaded during this one's scan: drawing chunks from per-pool ticket
+  // counters 269 us, since each atomic serialises at the memory side and its
+  // return stays in the wave's vmcnt, so every later wait also waits for it;
+  // a static round robin 188 us, its uneven per-wave totals leaving a 76 us
+  // tail; against 144 us for one chunk per wave.)
   const int nchunk = (nq + kWave - 1) / kWave;
   const int per = (nchunk + 7) / 8;
-  const int cx = (int)(blockIdx.x >> 3);
-  const int chunk = (int)(blockIdx.x & 7) * per + cx;
-  if (cx >= per || chunk >= nchunk) return;
+  const int pool = (int)(blockIdx.x & 7);
+  const int pend = min(nchunk, (pool + 1) * per);  // the pool's end
+  int chunk = pool * per + (int)(blockIdx.x >> 3);
+  if (chunk >= pend) return;
   const int lane = (int)threadIdx.x;
+  const uint32_t vmask = ~kKeyMask;
+  int bad = 0;  // an index that had to be clamped (a logic error)
+  // a chunk's per-lane inputs: the query's cell and index (cell-sorted),
+  // its block bounds in the row's list (k_nb_fill), its f64 point from the
+  // caller's cloud (issued after the bounds: only the scan needs it).
+  // (Carrying the points through the build instead, so that a chunk reads 64
+  // consecutive records, was measured in r5: the pass's raw FETCH 165 ->
+  // 105 MB and its time -3 us, the build +16-20 us.)
+  const int qc = min(chunk * kWave + lane, nq - 1);
+  const int qcell = QS.cell[qc], qidx = QS.idx[qc];
+  int ga, gb;
+  {
+    const bool lv = chunk * kWave + lane < nq;
+    const int row = lv ? qcell / g0 : 0;
+    const int x = lv ? qcell - row * g0 : 0;
+    ga = npg[row * (g0 + 1) + max(x - S, 0)];
+    gb = npg[row * (g0 + 1) + min(x + S + 1, g0)];
+  }
+  const double *qp = QS.pts + 3 * (size_t)qidx;
+  const double qv[3] = {qp[0], qp[1], qp[2]};
 #ifdef NAVGPU_STAMPS
   unsigned long long gst[8] = {__builtin_amdgcn_s_memrealtime(), 0, 0, 0, 0, 0, 0, 0};
 #endif
   const int nlive = min(kWave, nq - chunk * kWave);
   const int qi = chunk * kWave + lane;
   const bool live = lane < nlive;
-  const int qc = min(qi, nq - 1);
-  const int qcell = QS.cell[qc];
-  const int qidx = QS.idx[qc];
-  // the query's cell: x, row = (z g1 + y); rows ascend over the lanes
+  // the query's cell: x, row = (z g1 + y); rows ascend over the lanes.
+  // (Cell-sorted query records written by k_bin_fine were measured in r5:
+  // the query pass 142 -> 138 us, the build's gather of the points 115 ->
+  // 147 us.)
   const int qrow = live ? qcell / g0 : 0x7fffffff;
   const int qx = live ? qcell - qrow * g0 : 0;
-  const int rs = live ? qrow * (g0 + 1) : 0;
-  // the lane's block in its row's list (k_nb_fill), then its point (f64;
-  // issued after the block so the first wait does not cover it). (Cell-sorted
-  // query records written by k_bin_fine were measured in r5: the query pass
-  // 142 -> 138 us, but the build's gather of the points 115 -> 147 us.)
-  const int ga = npg[rs + max(qx - S, 0)];
-  const int gb = npg[rs + min(qx + S + 1, g0)];
-  const double *qp = QS.pts + 3 * (size_t)qidx;
-  const double qv[3] = {qp[0], qp[1], qp[2]};
-  const uint32_t vmask = ~kKeyMask;
-  int bad = 0;  // an index that had to be clamped (a logic error)
   const int prow = __shfl_up(qrow, 1, kWave), nrow = __shfl_down(qrow, 1, kWave);
   const unsigned long long rowfirst = __ballot(live && (lane == 0 || prow != qrow));
   const unsigned long long rowlast = __ballot(live && (lane == nlive - 1 || nrow != qrow));
@@ -2075,7 +1561,7 @@ __global__ __launch_bounds__(kWave, NAVGPU_KNNG_MINW) void k_knng(
 #pragma unroll
       for (int u = 0; u < kGU; ++u) {
         bad |= (unsigned)gpos[u] >= (unsigned)ntg;
-        rec[u] = *(const F3 *)&srec[min(max(gpos[u], 0), ntg - 1)];
+        rec[u] = *(const F3 *)&srec[min(max((kAbl & 8) ? (gpos[u] & 1023) : gpos[u], 0), ntg - 1)];
       }
 #pragma unroll
       for (int u = 0; u < kGU; ++u) {
@@ -2097,6 +1583,16 @@ __global__ __launch_bounds__(kWave, NAVGPU_KNNG_MINW) void k_knng(
 #endif
     // ---- the round's queries, one per lane (k_knnw's scan, exact stage and
     // certificate on the lane's block [t0, t1))
+    // a chunk done in one round, k = 8: its results leave through LDS, so
+    // that every store instruction writes whole 64-B (distances) and 32-B
+    // (indices) rows of 16 and 32 queries instead of 64 scattered 16-B
+    // pieces (r5 ablation: the direct stores cost ~18 us of the pass)
+    const bool tstore = K == 8 && L_.vec_out && la == 0 && lb == nlive && !(kAbl & 4);
+    // its LDS rows (over the dead image, each lane after its own reads of it):
+    // lane l's distances at 8 l doubles, indices after them, then its query
+    double *rd = (double *)spair;
+    int *ri = (int *)(rd + kWave * 8);
+    int *rq = ri + kWave * 8;
     if (in && lane < lb) {
       const int c[3] = {qx, qrow % g1, qrow / g1};
       const int t0 = pre + (ga - A), t1 = pre + (gb - A);
@@ -2166,9 +1662,9 @@ __global__ __launch_bounds__(kWave, NAVGPU_KNNG_MINW) void k_knng(
       NV_GT(ts2);
       NV_GADD(5, ts1, ts2);
       bool ok = !overflow && Dq < 1e17;
-      // exact f64 stage on the K best keys
       double ed[K];
       int ei[K];
+      // exact f64 stage on the K best keys
       if (key[0] != kNoKey) {
         int gq[K];
 #pragma unroll
@@ -2182,7 +1678,7 @@ __global__ __launch_bounds__(kWave, NAVGPU_KNNG_MINW) void k_knng(
 #pragma unroll
         for (int s = 0; s < K; ++s) {
           bad |= (unsigned)gq[s] >= (unsigned)ntg;
-          const PRec *tp = tsort + min(max(gq[s], 0), max(ntg - 1, 0));
+          const PRec *tp = tsort + min(max((kAbl & 1) ? (gq[s] & 1023) : gq[s], 0), max(ntg - 1, 0));
           gxy[s] = *(const double2 *)&tp->x;
           gzi[s] = *(const double2 *)&tp->z;
         }
@@ -2236,7 +1732,15 @@ __global__ __launch_bounds__(kWave, NAVGPU_KNNG_MINW) void k_knng(
         ok = ok && B > dk2 * (1.0 + 0x1p-46);
       else
         ok = ok && B == INFINITY;
-      if (ok) {
+      if (tstore) rq[lane] = ok ? qidx : -1;
+      if (ok && tstore) {
+#pragma unroll
+        for (int s = 0; s < K; s += 2)
+          *(double2 *)(rd + lane * 8 + s) = make_double2(ed[s], ed[s + 1]);
+#pragma unroll
+        for (int s = 0; s < K; s += 4)
+          *(int4 *)(ri + lane * 8 + s) = make_int4(ei[s], ei[s + 1], ei[s + 2], ei[s + 3]);
+      } else if (ok && (!(kAbl & 4) || ed[0] == -1.0)) {
         const size_t q = (size_t)qidx;
         if (K % 4 == 0 && L_.vec_out) {
 #pragma unroll
@@ -2252,16 +1756,37 @@ __global__ __launch_bounds__(kWave, NAVGPU_KNNG_MINW) void k_knng(
             odist[q * K + s] = ed[s];
           }
         }
-      } else {
+      } else if (!ok) {
         push_slow(L_, qi, (dk < INFINITY && !overflow) ? dk2 * (1.0 + 0x1p-46) : INFINITY);
       }
       NV_GT(ts3);
       NV_GADD(6, ts2, ts3);
     }
+    if (tstore) {
+      // (lanes outside the round: no row; written after every lane's reads
+      // of the image, which rq overlaps) then instruction i writes 16-B piece
+      // l & 3 of query 16 i + l / 4's distance row and piece l & 1 of query
+      // 32 i + l / 2's index row
+      if (!(in && lane < lb)) rq[lane] = -1;
+      wave_sync_mem();
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int qa = 16 * i + (lane >> 2), pc = lane & 3;
+        const int q = rq[qa];
+        const double2 v = *(const double2 *)(rd + qa * 8 + 2 * pc);
+        if (q >= 0) *(double2 *)(odist + (size_t)q * 8 + 2 * pc) = v;
+      }
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int qa = 32 * i + (lane >> 1), pc = lane & 1;
+        const int q = rq[qa];
+        const int4 v = *(const int4 *)(ri + qa * 8 + 4 * pc);
+        if (q >= 0) *(int4 *)(oidx + (size_t)q * 8 + 4 * pc) = v;
+      }
+    }
     la = lb;
     wave_sync_mem();  // LDS is restaged by the next round
   }
-  if (__any(bad) && lane == 0) atomicOr(L_.err, 1);
 #ifdef NAVGPU_STAMPS
   gst[1] = __builtin_amdgcn_s_memrealtime();
   gst[2] = __builtin_amdgcn_s_getreg((31 << 11) | 4);    // HW_REG_HW_ID
@@ -2280,6 +1805,7 @@ __global__ __launch_bounds__(kWave, NAVGPU_KNNG_MINW) void k_knng(
 #pragma unroll
     for (int i = 0; i < 8; ++i) g_gstamps[chunk][i] = gst[i];
 #endif
+  if (__any(bad) && lane == 0) atomicOr(L_.err, 1);
 }
 
 // ============================================================ k_knn_slow
@@ -2591,7 +2117,7 @@ static int knn_run(navgpu_ctx *ctx, const double *tgt, size_t nt, const double *
   const int nparts = (int)std::min<size_t>(kBBoxBlocks, std::max<size_t>(1, grid1d(nt, 256)));
   double *part;
   GridParams *gp;
-  int *tab, *tstart, *qstart, *bbase, *counters;
+  int *tab, *tstart, *bbase, *counters;
   BinPt *tbin = nullptr;
   QKey *qkey;
   int *qcell;
@@ -2602,7 +2128,6 @@ static int knn_run(navgpu_ctx *ctx, const double *tgt, size_t nt, const double *
   RC(ws(ctx, kParams, 1, &gp));
   RC(ws(ctx, kCnt, (size_t)ntab, &tab));
   RC(ws(ctx, kStart, nscan, &tstart));
-  RC(ws(ctx, kQStart, nscan, &qstart));
   int *btot;
   RC(ws(ctx, kBSum, 2 * (size_t)J.nb, &btot));
   RC(ws(ctx, kCellId, 2 * ((size_t)J.nb + 1), &bbase));
@@ -2630,7 +2155,7 @@ static int knn_run(navgpu_ctx *ctx, const double *tgt, size_t nt, const double *
   J.s[0].p = tgt;
   J.s[1].p = queries;
   J.s[0].start = tstart;
-  J.s[1].start = mode ? nullptr : qstart;  // k_knnw / k_knng read no query starts
+  J.s[1].start = nullptr;  // the query passes read no query cell starts
   J.s[0].bin = tbin;
   J.s[1].bin = nullptr;
   J.s[0].key = nullptr;
@@ -2695,17 +2220,10 @@ static int knn_run(navgpu_ctx *ctx, const double *tgt, size_t nt, const double *
   lists.err = counters + 2;
   lists.vec_out = ((uintptr_t)idx % 16 == 0 && (uintptr_t)dist % 16 == 0) ? 1 : 0;
   TimedRegion tr(ctx, "knn_query");
-  // tiles are walked by a grid of 8 x nbx blocks (block b -> XCD b % 8, the
-  // placement HW_REG_XCC_ID reports); more blocks than resident slots
-  // balance the uneven tiles
-  const int nbx = ctx->knn_blocks > 0
-                      ? ctx->knn_blocks
-                      : (int)std::min<size_t>(768, std::max<size_t>(1, nq / 1300 + 1));
-  const dim3 g(8 * nbx), b(kTileThreads);
   const dim3 gs(std::max<unsigned>(1, std::min<unsigned>(2048, grid1d(nq, 256))));
-  const float lambda = (float)ctx->knn_lambda;
-  // k_knnw: one 64-lane block per chunk of 64 cell-sorted queries, chunks
-  // dealt to the XCDs in contiguous ranges
+  // one 64-lane block per chunk of 64 cell-sorted queries, chunks dealt to
+  // the XCDs in contiguous ranges (block b -> XCD b % 8, the placement
+  // HW_REG_XCC_ID reports)
   const int nchunk = (int)((nq + kWave - 1) / kWave);
   const dim3 gw(8 * (((nchunk + 7) / 8 + kWPB - 1) / kWPB)), bw(kWave * kWPB);
   const QSide QS{queries, qperm, qcell};
@@ -2716,12 +2234,9 @@ static int knn_run(navgpu_ctx *ctx, const double *tgt, size_t nt, const double *
       hipLaunchKernelGGL((k_knng<KK>), gg, dim3(kWave), 0, s, gp, (const int *)npg,         \
                          (const int *)gl, (int)ngl, tsort, srec, QS, (int)nq, (int)nt, idx,  \
                          dist, lists);                                                      \
-    else if (mode == 1)                                                                     \
+    else                                                                                    \
       hipLaunchKernelGGL((k_knnw<KK>), gw, bw, 0, s, gp, tstart, tsort, srec, QS, (int)nq,      \
                          (int)nt, idx, dist, lists);                                        \
-    else                                                                                    \
-      hipLaunchKernelGGL((k_knn<KK>), g, b, 0, s, gp, tstart, tsort, qstart, QS,   \
-                         idx, dist, lists, lambda);                                         \
     hipLaunchKernelGGL((k_knn_slow<KK>), gs, dim3(256), 0, s, gp, tstart, tsort, QS,       \
                        idx, dist, lists);                                                   \
     break;

@@ -2872,8 +2872,7 @@ int navgpu_create(int device, void *stream, navgpu_ctx **out) {
   navgpu_ctx *c = new navgpu_ctx();
   c->device = device;
   if (const char *st = getenv("NAVGPU_KNN_STATS")) c->knn_stats = *st && *st != '0';
-  if (const char *o = getenv("NAVGPU_KNN_BLOCKS")) c->knn_blocks = atoi(o);
-  if (const char *o = getenv("NAVGPU_KNN_MODE")) c->knn_mode = std::min(std::max(atoi(o), 0), 2);
+  if (const char *o = getenv("NAVGPU_KNN_MODE")) c->knn_mode = std::min(std::max(atoi(o), 1), 2);
   if (const char *o = getenv("NAVGPU_KNN_SX")) {
     const int v = atoi(o);
     if (v >= 1 && v <= kKnnMaxSx) c->knn_sx = v;
@@ -2881,10 +2880,6 @@ int navgpu_create(int device, void *stream, navgpu_ctx **out) {
   if (const char *o = getenv("NAVGPU_KNN_OCC")) {
     const double v = atof(o);
     if (v > 0.05 && v < 1000) c->knn_occ = v;
-  }
-  if (const char *o = getenv("NAVGPU_KNN_LAMBDA")) {
-    const double v = atof(o);
-    if (v >= 1.0 && v < 1e6) c->knn_lambda = v;
   }
   if (stream) {
     c->stream = (hipStream_t)stream;

@@ -2,7 +2,7 @@
 # Build experimental libnavgpu variants (compile-time knobs, phase stamps,
 # timing-only ablations) into nav-slam_amd/lib/variants/ for
 # knn_probe.py --lib / knn_sweep.py.
-# usage: [VDIR=dir] scripts/build_variants.sh [name:"-DFLAG -DFLAG2" ...]  (default: stamps + k-NN ablations)
+# usage: [VDIR=dir] scripts/build_variants.sh [name:"-DFLAG -DFLAG2" ...]  (default: stamps)
 cd "$(dirname "$0")/.." || exit 1
 VDIR=${VDIR:-nav-slam_amd/lib/variants}
 rm -rf "$VDIR"; mkdir -p "$VDIR"
@@ -16,8 +16,6 @@ if [ $# -gt 0 ]; then
   for spec in "$@"; do build "${spec%%:*}" ${spec#*:}; done
 else
   build stamps -DNAVGPU_STAMPS
-  build noquery -DNAVGPU_ABL=1
-  build noexact -DNAVGPU_ABL=2
 fi
 wait
 ls "$VDIR"

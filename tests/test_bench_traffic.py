@@ -26,12 +26,12 @@ def _pmc_csv(path, counter, rows):
                         "Counter_Value": v})
 
 
-def _k3_passes(tmp_path, main="k_knn"):
+def _k3_passes(tmp_path, main="k_knnw"):
     knn = f"void (anonymous namespace)::{main}<8>((anonymous namespace)::GridParams const*)"
     slow = "void (anonymous namespace)::k_knn_slow<8>(int)"
     hist = "(anonymous namespace)::k_bin_hist((anonymous namespace)::BinJob)"
     f, w = str(tmp_path / "fetch.csv"), str(tmp_path / "write.csv")
-    # two steps: k_knn launched once per step
+    # two steps: the query pass launched once per step
     _pmc_csv(f, "FETCH_SIZE", [(1, hist, 10), (2, knn, 100), (3, slow, 4),
                                (4, hist, 12), (5, knn, 102), (6, slow, 2)])
     _pmc_csv(w, "WRITE_SIZE", [(1, hist, 1), (2, knn, 50), (3, slow, 1),
@@ -42,9 +42,9 @@ def _k3_passes(tmp_path, main="k_knn"):
 import pytest  # noqa: E402
 
 
-@pytest.mark.parametrize("main", ["k_knnw", "k_knn"])
+@pytest.mark.parametrize("main", ["k_knnw", "k_knng"])
 def test_pmc_bytes_per_step(tmp_path, main):
-    """k_knnw (r4 default) or k_knn (NAVGPU_KNN_MODE=0) is the per-step anchor."""
+    """k_knnw (NAVGPU_KNN_MODE=1) or k_knng (2) is the per-step anchor."""
     f, w = _k3_passes(tmp_path, main)
     q = bench.pmc_bytes([f, w], bench.QUERY_KERNELS)
     # fetch (100+4+102+2)/2 = 104 KB, write (50+1+52+1)/2 = 52 KB

@@ -22,6 +22,44 @@ def gpu():
     g.close()
 
 
+# every K3 query pass the library can select (NAVGPU_KNN_MODE): 1 k_knnw,
+# 2 k_knng on the row neighbourhood lists
+KNN_MODES = (1, 2)
+
+
+def _knn_ctx(mode, **env):
+    import os
+    from navslam.gpu import NavGpu
+    env = dict(env, NAVGPU_KNN_MODE=str(mode))
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
+    try:
+        return NavGpu(0)
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+
+
+@pytest.fixture(scope="module", params=KNN_MODES, ids=lambda m: f"mode{m}")
+def kgpu(request):
+    g = _knn_ctx(request.param)
+    yield g
+    g.close()
+
+
+_ORC_MEMO = {}
+
+
+def _memo(key, fn):
+    """oracle answers shared by the parametrised query passes"""
+    if key not in _ORC_MEMO:
+        _ORC_MEMO[key] = fn()
+    return _ORC_MEMO[key]
+
+
 def _eq(a, b, msg=""):
     a, b = np.asarray(a), np.asarray(b)
     if a.dtype.kind == "f":
@@ -489,7 +527,7 @@ def test_lazy_rows_vs_oracle(gpu, orc, seed, integer_mm, R, Cc):
 
 # ---------------------------------------------------------- global k-NN
 @pytest.mark.parametrize("k", [1, 3, 8, 16])
-def test_knn_vs_brute(gpu, orc, k):
+def test_knn_vs_brute(kgpu, orc, k):
     rng = np.random.default_rng(k)
     for tgt, q in [(rng.uniform(0, 1000, (5000, 3)), rng.uniform(-50, 1050, (3000, 3))),
                    (np.round(rng.uniform(0, 20, (4000, 3))), np.round(rng.uniform(0, 20, (2000, 3)))),
@@ -499,12 +537,12 @@ def test_knn_vs_brute(gpu, orc, k):
                     rng.uniform(0, 100, (500, 3))),                              # degenerate axis
                    (np.zeros((0, 3)), rng.uniform(0, 1, (10, 3)))]:               # empty target
         ri, rd = orc.knn_brute(tgt, q, k)
-        gi, gd = gpu.knn(tgt, q, k)
+        gi, gd = kgpu.knn(tgt, q, k)
         _eq(gi, ri, f"k={k} idx n={len(tgt)}")
         _eq(gd, rd, f"k={k} dist n={len(tgt)}")
 
 
-def test_knn_error_flag_stays_clear(gpu):
+def test_knn_error_flag_stays_clear(kgpu):
     """Every k-NN kernel clamps the list, cloud and record indices it loads
     through (so a logic error cannot fault the device) and flags the call
     when a clamp changed one (navgpu_knn_check -> NAVGPU_EINTERNAL). The
@@ -527,8 +565,8 @@ def test_knn_error_flag_stays_clear(gpu):
         for k in (1, 8):
             idx = torch.empty((len(q), k), dtype=torch.int32, device=dev)
             dst = torch.empty((len(q), k), dtype=torch.float64, device=dev)
-            gpu.knn_dev(tt if len(t) else qq, len(t), qq, len(q), k, idx, dst)
-            gpu.knn_check()
+            kgpu.knn_dev(tt if len(t) else qq, len(t), qq, len(q), k, idx, dst)
+            kgpu.knn_check()
 
 
 def _clustered(rng, n, centers, sigma, box):
@@ -538,7 +576,7 @@ def _clustered(rng, n, centers, sigma, box):
 
 
 @pytest.mark.parametrize("k", [1, 8])
-def test_knn_hard_cases(gpu, orc, k):
+def test_knn_hard_cases(kgpu, orc, k):
     """Inputs that leave the fast path: dense clusters (LDS-overflow tiles,
     runs longer than a key's offset field), non-finite coordinates, queries
     far outside the target box, a large common offset."""
@@ -568,18 +606,20 @@ def test_knn_hard_cases(gpu, orc, k):
     cases.append(("offset", t, q))
     for name, tgt, qs in cases:
         ri, rd = orc.knn_brute(tgt, qs, k)
-        gi, gd = gpu.knn(tgt, qs, k)
+        gi, gd = kgpu.knn(tgt, qs, k)
         _eq(gi, ri, f"{name} k={k} idx")
         _eq(gd, rd, f"{name} k={k} dist")
 
 
+@pytest.mark.parametrize("mode", KNN_MODES)
 @pytest.mark.parametrize("sx", [1, 2, 3, 8])
-def test_knn_cell_slicing_variants(orc, sx, monkeypatch):
+def test_knn_cell_slicing_variants(orc, sx, mode, monkeypatch):
     """NAVGPU_KNN_SX (x cells per h; default 3) reshapes every tile, block
     and certificate reach: each setting gives the brute-force answer, on
     uniform, integer-mm and clustered data, k = 2, 8 and 13."""
     from navslam.gpu import NavGpu
     monkeypatch.setenv("NAVGPU_KNN_SX", str(sx))
+    monkeypatch.setenv("NAVGPU_KNN_MODE", str(mode))
     g = NavGpu(0)
     try:
         rng = np.random.default_rng(40 + sx)
@@ -588,7 +628,7 @@ def test_knn_cell_slicing_variants(orc, sx, monkeypatch):
                  (_clustered(rng, 8000, 4, 1.0, 500.0), rng.uniform(0, 500, (1200, 3)))]
         for ci, (t, q) in enumerate(cases):
             for k in (2, 8, 13):
-                ri, rd = orc.knn_brute(t, q, k)
+                ri, rd = _memo(("sx", sx, ci, k), lambda: orc.knn_brute(t, q, k))
                 gi, gd = g.knn(t, q, k)
                 _eq(gi, ri, f"sx={sx} case {ci} k={k} idx")
                 _eq(gd, rd, f"sx={sx} case {ci} k={k} dist")
@@ -596,7 +636,7 @@ def test_knn_cell_slicing_variants(orc, sx, monkeypatch):
         g.close()
 
 
-def test_knn_huge_coordinates(gpu, orc):
+def test_knn_huge_coordinates(kgpu, orc):
     """Coordinates past the f32 offsets' certified range (|x| ~ 1e18 mm) and a
     cloud spanning 1e-3 .. 1e15 mm: the certificate fails and the slow path
     answers, exactly."""
@@ -604,43 +644,43 @@ def test_knn_huge_coordinates(gpu, orc):
     t = rng.uniform(-1, 1, (2000, 3)) * 1e18
     q = rng.uniform(-1, 1, (300, 3)) * 1e18
     ri, rd = orc.knn_brute(t, q, 8)
-    gi, gd = gpu.knn(t, q, 8)
+    gi, gd = kgpu.knn(t, q, 8)
     _eq(gi, ri, "1e18 idx")
     _eq(gd, rd, "1e18 dist")
     t = np.concatenate([rng.uniform(0, 1e-3, (1500, 3)), rng.uniform(0, 1e15, (1500, 3))])
     q = np.concatenate([rng.uniform(0, 1e-3, (200, 3)), rng.uniform(0, 1e15, (200, 3))])
     ri, rd = orc.knn_brute(t, q, 4)
-    gi, gd = gpu.knn(t, q, 4)
+    gi, gd = kgpu.knn(t, q, 4)
     _eq(gi, ri, "wide-range idx")
     _eq(gd, rd, "wide-range dist")
 
 
-def test_knn_k1_agrees_with_reference_kd_distances(gpu, golden):
+def test_knn_k1_agrees_with_reference_kd_distances(kgpu, golden):
     for pts, perm, q, nn, nnd in _golden_sets(golden("kdtree")):
         if len(pts) == 0:
             continue
-        gi, gd = gpu.knn(pts, q, 1)
+        gi, gd = kgpu.knn(pts, q, 1)
         _eq(gd[:, 0], nnd, "1-NN distance vs reference KD")
 
 
-def test_knn_k3_full_size_all_queries(gpu, orc):
+def test_knn_k3_full_size_all_queries(kgpu, orc):
     """K3 at full size (1M x 1M, k=8): EVERY query against the oracle's exact
     grid k-NN (orc_knn_grid, pinned to the brute force by test_oracle.py),
     plus a seeded sample of 1024 against the brute force itself."""
     from navslam.synth import uniform_pair
     src, tgt = uniform_pair(512, 2048)
-    gi, gd = gpu.knn(tgt, src, 8)
-    ri, rd = orc.knn_grid(tgt, src, 8)
+    gi, gd = kgpu.knn(tgt, src, 8)
+    ri, rd = _memo("k3", lambda: orc.knn_grid(tgt, src, 8))
     _eq(gi, ri, "all 1M queries: idx")
     _eq(gd, rd, "all 1M queries: dist")
     s = np.random.default_rng(9).choice(len(gi), 1024, replace=False)
-    bi, bd = orc.knn_brute(tgt, src.reshape(-1, 3)[s], 8)
+    bi, bd = _memo("k3b", lambda: orc.knn_brute(tgt, src.reshape(-1, 3)[s], 8))
     _eq(gi[s], bi, "sampled idx vs brute force")
     _eq(gd[s], bd, "sampled dist vs brute force")
 
 
 @pytest.mark.parametrize("integer_mm", [False, True])
-def test_knn_global_on_l9_scan(gpu, orc, integer_mm):
+def test_knn_global_on_l9_scan(kgpu, orc, integer_mm):
     """Global mode on a lidar-shaped pair instead of the uniform K3 cloud:
     points on surfaces (most grid cells empty, the rest dense), 2 % dropouts
     that all sit at (0, 0, 0) (utils/pointcloud.c:24-27: one cell holding
@@ -650,8 +690,8 @@ def test_knn_global_on_l9_scan(gpu, orc, integer_mm):
     from navslam.synth import l9_pair
     src, tgt = l9_pair(128, 2048, seed=21, integer_mm=integer_mm)
     for k in (1, 8):
-        gi, gd = gpu.knn(tgt, src, k)
-        ri, rd = orc.knn_grid(tgt, src, k)
+        gi, gd = kgpu.knn(tgt, src, k)
+        ri, rd = _memo(("l9", integer_mm, k), lambda: orc.knn_grid(tgt, src, k))
         _eq(gi, ri, f"l9 integer_mm={integer_mm} k={k}: idx")
         _eq(gd, rd, f"l9 integer_mm={integer_mm} k={k}: dist")
 
@@ -674,13 +714,13 @@ def _degenerate_clouds(name, rng):
 
 
 @pytest.mark.parametrize("name", ["line", "plane", "far_clusters"])
-def test_knn_global_degenerate_distributions(gpu, orc, name):
+def test_knn_global_degenerate_distributions(kgpu, orc, name):
     """Distributions the uniform grid handles worst (overflow tiles, overfull
     runs, a slow path for most queries, rings across empty space): every
     query against the oracle's exact grid k-NN, k = 8."""
     t, q = _degenerate_clouds(name, np.random.default_rng(5))
-    gi, gd = gpu.knn(t, q, 8)
-    ri, rd = orc.knn_grid(t, q, 8)
+    gi, gd = kgpu.knn(t, q, 8)
+    ri, rd = _memo(("degenerate", name), lambda: orc.knn_grid(t, q, 8))
     _eq(gi, ri, f"{name}: idx")
     _eq(gd, rd, f"{name}: dist")
 
@@ -692,7 +732,7 @@ def _digest_inputs_match(dg, prefix, src, tgt):
                     "digests were made from (numpy on this host generates other values)")
 
 
-def test_knn_k1_1m_matches_reference_kd_digest(gpu, golden):
+def test_knn_k1_1m_matches_reference_kd_digest(kgpu, golden):
     """the reference's own buildKDTree + nearestNeighborSearch over
     the 1M K3 pair (oracle/_ref, digests made by tests/golden/make_golden.py):
     the GPU's 1-NN points and distances hash to the same SHA-256."""
@@ -701,7 +741,7 @@ def test_knn_k1_1m_matches_reference_kd_digest(gpu, golden):
     dg = golden("digests")
     src, tgt = uniform_pair(512, 2048)
     _digest_inputs_match(dg, "k3", src, tgt)
-    gi, gd = gpu.knn(tgt, src, 1)
+    gi, gd = kgpu.knn(tgt, src, 1)
     pts, d = nn_digest_arrays(tgt.reshape(-1, 3), gi[:, 0], gd[:, 0])
     _eq(pts[:64], dg["k3_head_nn"], "first 64 nearest points")
     _eq(d[:64], dg["k3_head_nnd"], "first 64 distances")
@@ -1270,7 +1310,7 @@ def test_two_contexts_in_flight_match_one_at_a_time():
         c.close()
 
 
-def test_pair_knn_on_l9_scans_vs_oracle(gpu, orc):
+def test_pair_knn_on_l9_scans_vs_oracle(kgpu, orc):
     """The bench's pair entry point (navgpu_pair_knn_dev: curvature of both
     clouds on a side stream + global k-NN) on lidar-shaped scans: masks
     against the oracle's extract_feature (src/slam.c:11-61) and every query
@@ -1285,10 +1325,11 @@ def test_pair_knn_on_l9_scans_vs_oracle(gpu, orc):
     tm = torch.empty((R, Cc), dtype=torch.int32, device=dev)
     idx = torch.empty((R * Cc, k), dtype=torch.int32, device=dev)
     dst = torch.empty((R * Cc, k), dtype=torch.float64, device=dev)
-    gpu.pair_knn_dev(s, t, R, Cc, k, sm, tm, idx, dst)
+    kgpu.pair_knn_dev(s, t, R, Cc, k, sm, tm, idx, dst)
     torch.cuda.synchronize()
+    kgpu.knn_check()
     _eq(sm.cpu().numpy(), orc.extract_feature(src), "src mask")
     _eq(tm.cpu().numpy(), orc.extract_feature(tgt), "tgt mask")
-    ri, rd = orc.knn_grid(tgt, src, k)
+    ri, rd = _memo("pair_l9", lambda: orc.knn_grid(tgt, src, k))
     _eq(idx.cpu().numpy(), ri, "idx")
     _eq(dst.cpu().numpy(), rd, "dist")
