@@ -144,15 +144,22 @@ int navgpu_kd_query_rows_dev(navgpu_ctx *ctx, const double *tree_pts,
  * would), with all their queries walked. nn_pos indexes the row as it is on
  * return (column order for untied rows). For a caller that needs no host
  * KDNode trees (the shim with NAVSLAM_HOST_TREES=0): the per-row Lomuto
- * chain (utils/kdtree.c:20-82) runs only for tied rows. */
+ * chain (utils/kdtree.c:20-82) runs only for tied rows. tree_built (device,
+ * R ints, nullable; zeroed by the compaction): 1 for a row the lazy query has
+ * already turned into the reference tree, so that a second lazy query over
+ * the same rows (two localisations between mappings) walks that tree instead
+ * of rebuilding it from an order that is no longer the column order. NULL:
+ * the caller re-compacts before every lazy query. */
 int navgpu_kd_compact_rows_dev(navgpu_ctx *ctx, const double *feat_src,
                                const double *coords, int R, int C,
                                double *tree_pts, int32_t *tree_col,
-                               int32_t *tree_n, int32_t *mask_out);
+                               int32_t *tree_n, int32_t *mask_out,
+                               int32_t *tree_built);
 int navgpu_kd_query_rows_lazy_dev(navgpu_ctx *ctx, double *tree_pts, int32_t *tree_col,
                                   const int32_t *tree_n, const double *feat_src,
                                   const double *queries, int R, int C, int32_t *nn_pos,
-                                  double *nn_dist, int32_t *mask_out);
+                                  double *nn_dist, int32_t *mask_out,
+                                  int32_t *tree_built);
 
 /* ---- R7: correspondence dedup per row (src/slam.c:247-284) -------------
  * Over the output of navgpu_kd_query_rows: of the queries of row r whose

@@ -916,6 +916,11 @@ __device__ unsigned long long g_wstamps[kWStampChunks][8];
 #define NV_WFLUSH(chunk)
 #endif
 
+// k_knnw asks for 4 waves per SIMD; its LDS allows 3, so the backend reports
+// the occupancy target as missed ("pass failed"); the request still measured
+// faster (r4), and only this kernel's warning is silenced
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Wpass-failed"
 template <int K>
 __global__ __launch_bounds__(kWave * kWPB, NAVGPU_KNNW_MINW) void k_knnw(const GridParams *__restrict__ gp,
                                                    const int *__restrict__ tstart,
@@ -1378,6 +1383,7 @@ __global__ __launch_bounds__(kWave * kWPB, NAVGPU_KNNW_MINW) void k_knnw(const G
   NV_ACC(8, w0, w9);
   NV_WFLUSH(chunk);
 }
+#pragma clang diagnostic pop
 
 // ============================================================ k_knng
 // The query pass on the row neighbourhood lists (r5, default): one WAVE per

@@ -140,8 +140,11 @@ __device__ __forceinline__ int tape_jump(int p, int sp, unsigned long long lbelo
                                          int wave_p0) {
   const int k = p - sp;  // >= 1
   const int s = lbelow ? wave_p0 + kWave - __clzll(lbelow) : wave_p0;
-  // (p - s + k) / k exactly: the f32 reciprocal's quotient is within one of
-  // it for operands below 2^24, then one correction (no integer divide)
+  // (p - s + k) / k exactly, with no integer divide: the f32 quotient
+  // a * rcp(k) has a relative error below 2^-22 (rcp 1 ulp, two roundings),
+  // so it is within one of a / k while a / k < 2^22, which holds for every
+  // caller (positions are 16-bit: rows and LDS windows below 2^16, a < 2^17);
+  // then one correction
   const int a = p - s + k;
   int q = (int)((float)a * __builtin_amdgcn_rcpf((float)k));
   const int r = a - q * k;
@@ -1981,7 +1984,8 @@ __global__ __launch_bounds__(NT) void k_rows_query_screen(
     const double *__restrict__ tree_pts, const int32_t *__restrict__ tree_n,
     const double *__restrict__ feat_src, const double *__restrict__ queries, int R, int C,
     int32_t *__restrict__ nn_pos, double *__restrict__ nn_dist, int32_t *__restrict__ mask_out,
-    int32_t *__restrict__ tie, const int32_t *__restrict__ tree_col) {
+    int32_t *__restrict__ tie, const int32_t *__restrict__ tree_col,
+    const int32_t *__restrict__ built) {
   const int r = blockIdx.x;
   const int w = (C + (int)gridDim.y - 1) / (int)gridDim.y;
   const int c0 = (int)blockIdx.y * w, c1 = min(C, c0 + w);
@@ -1998,9 +2002,12 @@ __global__ __launch_bounds__(NT) void k_rows_query_screen(
   int *scan = (int *)((unsigned char *)FL + align16(2 * w));
   uint32_t *stk = (uint32_t *)((unsigned char *)scan + align16(4 * 40));
   // lazy rows (column order, no tree): the walk stack's region holds the
-  // rows' feature columns instead (no query walks here)
+  // rows' feature columns instead (no query walks here). A lazy row an
+  // earlier call already rebuilt (built[r]) holds the reference tree: it is
+  // screened and walked as a built one.
   uint16_t *TCOL = (uint16_t *)stk;
-  const bool lazy = tree_col != nullptr;
+  const bool rowbuilt = built && built[r];
+  const bool lazy = tree_col != nullptr && !rowbuilt;
   const int n = tree_n[r];
   const int nch = (n + kScreenChunk - 1) / kScreenChunk;
   for (int pos = threadIdx.x; pos < nch * kScreenChunk; pos += NT) {
@@ -2102,7 +2109,7 @@ __global__ __launch_bounds__(NT) void k_rows_query_screen(
       double bd = j1 >= 0 ? dist : INFINITY;
       const bool under = d1 < INFINITY && dist > 0.0 && dist < 1e-150;
       if (genuine || under) {
-        if (tie) {  // the row holds no tree yet: k_rows_retree walks all its queries
+        if (lazy) {  // the row holds no tree yet: k_rows_retree walks all its queries
           tie[r] = 1;
           bd = under ? -1.0 : bd;  // its walk's stop distance (-1: the whole walk)
         } else {
@@ -2126,9 +2133,9 @@ __global__ __launch_bounds__(kRowsBlock) void k_rows_retree(
     double *__restrict__ tree_pts, int32_t *__restrict__ tree_col,
     const int32_t *__restrict__ tree_n, const double *__restrict__ feat_src,
     const double *__restrict__ queries, int C, int32_t *__restrict__ nn_pos,
-    double *__restrict__ nn_dist, const int32_t *__restrict__ tie) {
+    double *__restrict__ nn_dist, const int32_t *__restrict__ tie, int32_t *__restrict__ built) {
   const int r = blockIdx.x;
-  if (!tie[r]) return;  // uniform
+  if (!tie[r]) return;  // uniform (a built row's ties were walked by the screen)
   const RowsLds L = rows_lds(C, kRowsBlock, true);
   const size_t rowoff = (size_t)r * C;
   const int n = tree_n[r];
@@ -2165,6 +2172,7 @@ __global__ __launch_bounds__(kRowsBlock) void k_rows_retree(
     o[2] = TZ[pos];
     tree_col[rowoff + pos] = T[pos];
   }
+  if (built && threadIdx.x == 0) built[r] = 1;  // a later lazy query walks this tree
   // the query row's features (its curvature, src/slam.c:11-61) -> the walk
   double *sraw = FC;
   uint16_t *SM = P;
@@ -3178,7 +3186,10 @@ int navgpu_kd_build_rows_dev(navgpu_ctx *ctx, const double *feat_src,
 int navgpu_kd_compact_rows_dev(navgpu_ctx *ctx, const double *feat_src,
                                const double *coords, int R, int C,
                                double *tree_pts, int32_t *tree_col,
-                               int32_t *tree_n, int32_t *mask_out) {
+                               int32_t *tree_n, int32_t *mask_out, int32_t *tree_built) {
+  ARG_CHECK(ctx && R >= 0);
+  if (tree_built && R > 0)  // every row back in column order
+    HIP_TRY(hipMemsetAsync(tree_built, 0, 4 * (size_t)R, ctx->stream));
   return rows_build_launch(ctx, feat_src, coords, R, C, tree_pts, tree_col, tree_n, mask_out, 0);
 }
 
@@ -3250,7 +3261,8 @@ static int rows_query_launch(navgpu_ctx *ctx, const double *tree_pts,
                              const double *queries, int R, int C,
                              int32_t *nn_pos, double *nn_dist,
                              int32_t *mask_out, int32_t *tie,
-                             const int32_t *tree_col = nullptr) {
+                             const int32_t *tree_col = nullptr,
+                             const int32_t *built = nullptr) {
   ARG_CHECK(ctx);
   RC(check_rows_shape(R, C, true));
   if ((size_t)R * C == 0) return NAVGPU_OK;
@@ -3275,7 +3287,7 @@ static int rows_query_launch(navgpu_ctx *ctx, const double *tree_pts,
     TimedRegion tr(ctx, "rows_query");
     hipLaunchKernelGGL(k_rows_query_screen<kRowsQBlock>, dim3(R, S), dim3(kRowsQBlock), lds,
                        ctx->stream, tree_pts, tree_n, feat_src, queries, R, C, nn_pos, nn_dist,
-                       mask_out, tie, tie ? tree_col : nullptr);
+                       mask_out, tie, tie ? tree_col : nullptr, tie ? built : nullptr);
     CHECK_LAUNCH("k_rows_query_screen");
     return NAVGPU_OK;
   }
@@ -3310,7 +3322,7 @@ int navgpu_kd_query_rows_dev(navgpu_ctx *ctx, const double *tree_pts,
 int navgpu_kd_query_rows_lazy_dev(navgpu_ctx *ctx, double *tree_pts, int32_t *tree_col,
                                   const int32_t *tree_n, const double *feat_src,
                                   const double *queries, int R, int C, int32_t *nn_pos,
-                                  double *nn_dist, int32_t *mask_out) {
+                                  double *nn_dist, int32_t *mask_out, int32_t *tree_built) {
   ARG_CHECK(ctx);
   RC(check_rows_shape(R, C, true));
   if ((size_t)R * C == 0) return NAVGPU_OK;
@@ -3319,7 +3331,7 @@ int navgpu_kd_query_rows_lazy_dev(navgpu_ctx *ctx, double *tree_pts, int32_t *tr
   RC(ws(ctx, kRowTie, (size_t)R, &tie));
   HIP_TRY(hipMemsetAsync(tie, 0, 4 * (size_t)R, ctx->stream));
   RC(rows_query_launch(ctx, tree_pts, tree_n, feat_src, queries, R, C, nn_pos, nn_dist,
-                       mask_out, tie, tree_col));
+                       mask_out, tie, tree_col, tree_built));
   const RowsLds L = rows_lds(C, kRowsBlock, true);
   if (L.total > lds_limit()) {
     set_err("rows_query_lazy: C=%d needs %d B of LDS (device limit %d)", C, L.total,
@@ -3330,7 +3342,7 @@ int navgpu_kd_query_rows_lazy_dev(navgpu_ctx *ctx, double *tree_pts, int32_t *tr
   TimedRegion tr(ctx, "rows_retree");
   hipLaunchKernelGGL(k_rows_retree, dim3(R), dim3(kRowsBlock), L.total, ctx->stream, tree_pts,
                      tree_col, tree_n, feat_src, queries, C, nn_pos, nn_dist,
-                     (const int32_t *)tie);
+                     (const int32_t *)tie, tree_built);
   CHECK_LAUNCH("k_rows_retree");
   return NAVGPU_OK;
 }

@@ -324,6 +324,7 @@ typedef struct {
     double *d_lidar, *d_global, *d_last, *d_tree, *d_dist, *d_sums, *d_list;
     double h_sums[6 * ROWS];
     int32_t *d_tcol, *d_tn, *d_pos, *d_count;
+    int32_t *d_built; /* lazy rows already turned into the reference tree */
     int have_trees;
     int lazy; /* the rows hold compacted features, trees only where ties need them */
     double prof_t0; /* NAVSLAM_PROFILE */
@@ -357,6 +358,7 @@ static slam_state *state_for(SLAM_attr *a)
     CK(navgpu_malloc(c, 8 * NPTS, (void **)&s->d_dist));
     CK(navgpu_malloc(c, 4 * NPTS, (void **)&s->d_tcol));
     CK(navgpu_malloc(c, 4 * ROWS, (void **)&s->d_tn));
+    CK(navgpu_malloc(c, 4 * ROWS, (void **)&s->d_built));
     CK(navgpu_malloc(c, 4 * NPTS, (void **)&s->d_pos));
     CK(navgpu_malloc(c, 8 * 6 * ROWS, (void **)&s->d_sums));
     CK(navgpu_malloc(c, 56 * (size_t)NPTS, (void **)&s->d_list));
@@ -415,7 +417,7 @@ static void map_frame(SLAM_attr *attr, slam_state *s, Pos pos,
     s->lazy = !host_trees();
     if (s->lazy)
         CK(navgpu_kd_compact_rows_dev(c, s->d_lidar, s->d_global, ROWS, COLS,
-                                      s->d_tree, s->d_tcol, s->d_tn, NULL));
+                                      s->d_tree, s->d_tcol, s->d_tn, NULL, s->d_built));
     else
         CK(navgpu_kd_build_rows_dev(c, s->d_lidar, s->d_global, ROWS, COLS,
                                     s->d_tree, s->d_tcol, s->d_tn, NULL));
@@ -591,7 +593,8 @@ Pos slam_localization(SLAM_attr *attr, PointCloud *lidarPointCloud,
     }
     if (s->lazy)
         CK(navgpu_kd_query_rows_lazy_dev(c, s->d_tree, s->d_tcol, s->d_tn, s->d_lidar,
-                                         s->d_last, ROWS, COLS, s->d_pos, s->d_dist, NULL));
+                                         s->d_last, ROWS, COLS, s->d_pos, s->d_dist, NULL,
+                                         s->d_built));
     else
         CK(navgpu_kd_query_rows_dev(c, s->d_tree, s->d_tn, s->d_lidar, s->d_last,
                                     ROWS, COLS, s->d_pos, s->d_dist, NULL));

@@ -46,9 +46,9 @@ def _declare(L):
         "navgpu_kd_query_rows_dev": (C.c_int, [_vp, _vp, _vp, _vp, _vp, C.c_int,
                                                C.c_int, _vp, _vp, _vp]),
         "navgpu_kd_compact_rows_dev": (C.c_int, [_vp, _vp, _vp, C.c_int, C.c_int,
-                                                 _vp, _vp, _vp, _vp]),
+                                                 _vp, _vp, _vp, _vp, _vp]),
         "navgpu_kd_query_rows_lazy_dev": (C.c_int, [_vp, _vp, _vp, _vp, _vp, _vp,
-                                                    C.c_int, C.c_int, _vp, _vp, _vp]),
+                                                    C.c_int, C.c_int, _vp, _vp, _vp, _vp]),
         "navgpu_rows_corr_dev": (C.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, C.c_int,
                                            C.c_int, _vp, _vp]),
         "navgpu_rows_corr_list_dev": (C.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, C.c_int,
@@ -283,16 +283,16 @@ class NavGpu:
             _ptr(nn_pos), _ptr(nn_dist), _ptr(mask)), "kd_query_rows_dev")
 
     def kd_compact_rows_dev(self, feat_src, coords, R, Cc, tree_pts, tree_col, tree_n,
-                            mask=None):
+                            mask=None, built=None):
         self._check(self.L.navgpu_kd_compact_rows_dev(
             self.h, _ptr(feat_src), _ptr(coords), R, Cc, _ptr(tree_pts), _ptr(tree_col),
-            _ptr(tree_n), _ptr(mask)), "kd_compact_rows_dev")
+            _ptr(tree_n), _ptr(mask), _ptr(built)), "kd_compact_rows_dev")
 
     def kd_query_rows_lazy_dev(self, tree_pts, tree_col, tree_n, feat_src, queries, R, Cc,
-                               nn_pos, nn_dist, mask=None):
+                               nn_pos, nn_dist, mask=None, built=None):
         self._check(self.L.navgpu_kd_query_rows_lazy_dev(
             self.h, _ptr(tree_pts), _ptr(tree_col), _ptr(tree_n), _ptr(feat_src),
-            _ptr(queries), R, Cc, _ptr(nn_pos), _ptr(nn_dist), _ptr(mask)),
+            _ptr(queries), R, Cc, _ptr(nn_pos), _ptr(nn_dist), _ptr(mask), _ptr(built)),
             "kd_query_rows_lazy_dev")
 
     def rows_corr_dev(self, tree_pts, tree_n, nn_pos, nn_dist, ori, R, Cc, keep, sums):

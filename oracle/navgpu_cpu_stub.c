@@ -166,9 +166,12 @@ int navgpu_kd_build_rows_dev(navgpu_ctx *ctx, const double *feat_src, const doub
 /* compacted rows in column order (no permutation) */
 int navgpu_kd_compact_rows_dev(navgpu_ctx *ctx, const double *feat_src, const double *coords,
                                int R, int C, double *tree_pts, int32_t *tree_col,
-                               int32_t *tree_n, int32_t *mask_out)
+                               int32_t *tree_n, int32_t *mask_out, int32_t *tree_built)
 {
     (void)ctx;
+    if (tree_built)
+        for (int r = 0; r < R; r++)
+            tree_built[r] = 0;
     const size_t N = (size_t)R * C;
     int *feat = malloc(sizeof(int) * (N ? N : 1));
     int *cols = malloc(sizeof(int) * (C ? C : 1));
@@ -354,16 +357,22 @@ int navgpu_rows_corr_dev(navgpu_ctx *ctx, const double *tree_pts, const int32_t 
 }
 
 /* the lazy query: here every row gets its tree (the device builds only the
- * rows with a tie; the answers' coordinates are the same either way) */
+ * rows with a tie; the answers' coordinates are the same either way), once:
+ * a row tree_built marks already holds it */
 int navgpu_kd_query_rows_lazy_dev(navgpu_ctx *ctx, double *tree_pts, int32_t *tree_col,
                                   const int32_t *tree_n, const double *feat_src,
                                   const double *queries, int R, int C, int32_t *nn_pos,
-                                  double *nn_dist, int32_t *mask_out)
+                                  double *nn_dist, int32_t *mask_out, int32_t *tree_built)
 {
     int *cols = malloc(sizeof(int) * (C ? C : 1));
     if (!cols)
         return NAVGPU_ENOMEM;
     for (int r = 0; r < R; r++) {
+        if (tree_built) {
+            if (tree_built[r])
+                continue;
+            tree_built[r] = 1;
+        }
         for (int i = 0; i < tree_n[r]; i++)
             cols[i] = tree_col[(size_t)r * C + i];
         orc_kd_build(tree_pts + 3 * (size_t)r * C, cols, (size_t)tree_n[r]);

@@ -491,12 +491,27 @@ def test_lazy_rows_vs_oracle(gpu, orc, seed, integer_mm, R, Cc):
     tcol = torch.zeros((R, Cc), dtype=torch.int32, device=dev)
     tn = torch.zeros(R, dtype=torch.int32, device=dev)
     mask = torch.zeros((R, Cc), dtype=torch.int32, device=dev)
-    gpu.kd_compact_rows_dev(d_lid, d_coords, R, Cc, tree, tcol, tn, mask)
     pos = torch.zeros((R, Cc), dtype=torch.int32, device=dev)
     dist = torch.zeros((R, Cc), dtype=torch.float64, device=dev)
     qmask = torch.zeros((R, Cc), dtype=torch.int32, device=dev)
-    gpu.kd_query_rows_lazy_dev(tree, tcol, tn, d_lid2, d_lid2, R, Cc, pos, dist, qmask)
+    built = torch.full((R,), 7, dtype=torch.int32, device=dev)  # compaction zeroes it
+    pos2 = torch.zeros_like(pos)
+    dist2 = torch.zeros_like(dist)
+    torch.cuda.synchronize()  # (the library runs on its own stream)
+    gpu.kd_compact_rows_dev(d_lid, d_coords, R, Cc, tree, tcol, tn, mask, built)
+    gpu.kd_query_rows_lazy_dev(tree, tcol, tn, d_lid2, d_lid2, R, Cc, pos, dist, qmask, built)
     gpu.sync()
+    # a second lazy query over the same rows: rows the first one
+    # rebuilt are walked as they stand, not rebuilt again; same answers
+    tree1, tcol1 = tree.clone(), tcol.clone()
+    torch.cuda.synchronize()
+    gpu.kd_query_rows_lazy_dev(tree, tcol, tn, d_lid2, d_lid2, R, Cc, pos2, dist2, None, built)
+    gpu.sync()
+    _eq(tree.cpu().numpy(), tree1.cpu().numpy(), "second lazy query: rows unchanged")
+    _eq(tcol.cpu().numpy(), tcol1.cpu().numpy(), "second lazy query: columns unchanged")
+    _eq(pos2.cpu().numpy(), pos.cpu().numpy(), "second lazy query: positions")
+    _eq(dist2.cpu().numpy(), dist.cpu().numpy(), "second lazy query: distances")
+    nb = built.cpu().numpy()
     fm = orc.extract_feature(lid)
     _eq(mask.cpu().numpy(), fm, "build mask")
     qm = orc.extract_feature(lid2)
@@ -510,8 +525,10 @@ def test_lazy_rows_vs_oracle(gpu, orc, seed, integer_mm, R, Cc):
         assert tn[r] == n
         rt, rix = orc.kd_build(coords[r, cols])
         if (tcol[r, :n] == cols).all() and tree[r, :n].tobytes() == coords[r, cols].tobytes():
-            pass  # left in column order
+            # left in column order (or rebuilt into a tree that is that order)
+            assert nb[r] == 0 or rt.tobytes() == coords[r, cols].tobytes(), r
         else:
+            assert nb[r] == 1, r
             rebuilt += 1
             _eq(tree[r, :n], rt, f"row {r} rebuilt tree")
             _eq(tcol[r, :n], cols[rix], f"row {r} rebuilt cols")
@@ -949,6 +966,41 @@ def test_shim_l9_stream_vs_oracle(monkeypatch, R, Cc, F, steps, trees):
         assert q >= cp
         last_g, last_o = meas, om
     assert attr.frameCount == s.frame_count
+
+
+@pytest.mark.parametrize("trees", ["1", "0"])
+def test_shim_localise_twice_between_mappings(monkeypatch, trees):
+    """Two localisations against the same map (no slam_mapping between them,
+    a caller the reference allows): with lazy rows (NAVSLAM_HOST_TREES=0) the
+    first call turns tied rows into the reference tree in place, and the
+    second must walk that tree, not rebuild one from the permuted order
+    (ADVICE r4). Integer-mm frames make ties common. Every pose and error
+    against the oracle's slam.c, for host trees on and off."""
+    monkeypatch.setenv("NAVSLAM_QUIET", "1")
+    monkeypatch.setenv("NAVSLAM_HOST_TREES", trees)
+    from pyoracle import Oracle, OracleSlam
+    from shimlib import Pos, Shim
+    from navslam.synth import l9_stream
+    R, Cc, F = 128, 2048, 4
+    frames = l9_stream(R, Cc, F, seed=29, integer_mm=True)
+    sh = Shim(R, Cc)
+    attr = sh.SLAMAttr()
+    pcs = [sh.cloud(f) for f in frames]
+    zero = np.zeros(6)
+    sh.L.init_slam(C.byref(attr), Pos.of(zero), C.byref(pcs[0]))
+    orc = Oracle()
+    s = OracleSlam(orc, R, Cc)
+    s.init(zero, frames[0])
+    last_g, last_o = Pos.of(zero), zero
+    for f in range(1, F):
+        for rep in range(2):  # the same map twice; the second starts at the first's answer
+            meas = sh.L.slam_localization(C.byref(attr), C.byref(pcs[f]), last_g, last_g)
+            om, _, _ = s.localization(frames[f], last_o, last_o)
+            _eq(np.array(meas.tolist()), om, f"frame {f} localisation {rep} pose")
+            assert attr.error == s.error, f"frame {f} localisation {rep} error"
+            last_g, last_o = meas, om
+        sh.L.slam_mapping(C.byref(attr), meas, C.byref(pcs[f]))
+        s.mapping(om, frames[f])
 
 
 def _dedup_reference(orc, tree, pos, dist, ori):
