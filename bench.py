@@ -282,6 +282,11 @@ def run_k5(a, ws, rank, dev):
     sh = Shim(R, Cc)
     pcs = [sh.cloud(frames[f], ts=f) for f in range(F)]
     attr = sh.SLAMAttr()
+    # the caller's SLAM_attr (100 map slots, 630 MB at 128 x 2048) touched once
+    # before timing: a long run writes every slot many times, so a short
+    # timed run must not pay the first-touch page faults of 60 fresh slots
+    import ctypes
+    ctypes.memset(ctypes.addressof(attr), 0, ctypes.sizeof(attr))
     zero = Pos.of([0.0] * 6)
     sh.L.init_slam(attr, zero, pcs[0])
     poses, state = [], {"i": 0, "last": zero, "q": 0}
@@ -329,6 +334,7 @@ def run_k5(a, ws, rank, dev):
     frames_all = shard.sum_over_ranks(a.steps, dev)
     if rank != 0:
         return None
+    floor = k5_copy_floor(L, ctx, pcs, attr, R * Cc)
     cpu = None
     if not a.no_cpu_baseline and a.cpu_frames > 0:
         cpu = cpu_baseline_k5(frames, F, min(a.cpu_frames, len(poses)), poses)
@@ -371,8 +377,48 @@ def run_k5(a, ws, rank, dev):
                       "queries_per_frame": round(qpf, 1), "mode": "rows"},
            "roofline": roof, "curvature_plus_query": None,
            "kernel_us": {n: round(per_frame(n), 2) for n in names},
+           # the frame's API copies alone (the same pageable frame and map-slot
+           # buffers, the same entry points, nothing else on the device): the
+           # floor a frame of this API cannot go below
+           "copy_floor_ms": round(floor["ms"], 4),
+           "copy_floor": floor,
+           "frac_of_copy_floor": round(floor["ms"] / (1000.0 * elapsed / a.steps), 4),
            "cpu_baseline": cpu}
     return out
+
+
+def k5_copy_floor(L, ctx, pcs, attr, npts, reps=20):
+    """Per-frame floor of the K5 API's host copies: the frame uploaded twice
+    (slam_localization and slam_mapping each upload their lidar cloud) and
+    the 24 B/point map slot downloaded once, timed alone over `reps` frames
+    with the same pageable buffers and navgpu_upload/download."""
+    import ctypes
+    nb = 24 * npts
+    d = ctypes.c_void_p()
+    if L.navgpu_malloc(ctx, nb, ctypes.byref(d)) != 0:
+        raise RuntimeError("k5_copy_floor: device allocation failed")
+    try:
+        src = ctypes.addressof(pcs[0].pos)
+        dst = ctypes.addressof(attr.globalPointCloud[0].pos)
+        t = {"h2d": 0.0, "d2h": 0.0}
+        for rep in range(reps + 2):  # two warm-up frames
+            a0 = time.perf_counter()
+            for _ in range(2):
+                L.navgpu_upload(ctx, d, src, nb)
+            L.navgpu_sync(ctx)
+            a1 = time.perf_counter()
+            L.navgpu_download(ctx, dst, d, nb)
+            L.navgpu_sync(ctx)
+            a2 = time.perf_counter()
+            if rep >= 2:
+                t["h2d"] += a1 - a0
+                t["d2h"] += a2 - a1
+    finally:
+        L.navgpu_free(ctx, d)
+    h2d, d2h = 1000.0 * t["h2d"] / reps, 1000.0 * t["d2h"] / reps
+    return {"ms": h2d + d2h, "h2d_ms_2x": round(h2d, 4), "d2h_ms": round(d2h, 4),
+            "bytes": 3 * nb, "gbs": round(3 * nb / ((h2d + d2h) * 1e-3) / 1e9, 2),
+            "buffers": "pageable (the frame's PointCloud, the map slot)"}
 
 
 def cpu_baseline_k5(frames, F, nf, gpu_poses):
@@ -506,6 +552,7 @@ def main():
             data = data.replace(f"{npairs} distinct pairs j resident and rotated per step",
                                 "one resident pair replayed by a hipGraph")
         cfg_extra = {"points_per_cloud": N, "k": a.k, "pairs_per_gpu": 1, "mode": "global",
+                     "knn_mode": knn_mode(), "query_kernel": knn_query_kernel(),
                      "pairs_in_flight": nf, "resident_pairs": res_pairs,
                      "resident_bytes": res_pairs * 2 * 24 * N}
     else:
@@ -694,15 +741,25 @@ def main():
                     build_traffic = tj.get("build_bytes_per_step")
             roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
                     "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic,
+                    # where traffic comes from: this run's PMC CSVs (--traffic-csv),
+                    # or the committed json of the round's profiling session
+                    "traffic_measured_in_run": bool(a.traffic_csv),
                     "kernel": ("query stage %s<%d> + k_knn_slow<%d>, one launch each per "
-                               "step" % ("k_knn" if os.environ.get("NAVGPU_KNN_MODE") == "0"
-                                         else "k_knnw", a.k, a.k)),
+                               "step" % (knn_query_kernel(), a.k, a.k)),
                     "avg_us": round(dom_avg_us, 2), "launches": dom_n,
                     "timing": ("HIP events on each context's stream over the timed region"
-                               + (f" ({nf} pairs in flight: shares the chip with the other "
-                                  "pair's build)" if nf > 1 else "")),
+                               + (f" ({nf} pairs in flight: a contended span that also holds "
+                                  "the other pair's interleaved kernels)" if nf > 1 else "")),
                     "bytes_per_launch": dom_bytes,
                     "bytes_model": "24 B/query read + 24 B/target read + 12*k B/query out"}
+            tr = load_trace(a, {"k": a.k, "points_per_cloud": N, "knn_mode": knn_mode()})
+            if tr is not None and tr.get("trace_us", {}).get("knn_query"):
+                # the trace basis (r5): the query stage's kernel
+                # durations per launch in the rocprofv3 trace of this command
+                q_us = tr["trace_us"]["knn_query"]
+                roof["trace"] = {"query_stage_us": q_us, "main_kernel_us": tr.get("main_avg_us"),
+                                 "frac": round(dom_bytes / (q_us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),
+                                 "source": tr.get("source"), "measured_in_run": False}
             if kt_iso is not None and kt_iso.get(dom, (0, 0))[1] > 0:
                 iso_us = 1000.0 * kt_iso[dom][0] / kt_iso[dom][1]
                 roof["avg_us_isolated"] = round(iso_us, 2)
@@ -819,6 +876,35 @@ def traffic_tag(a):
     if a.workload == "k5" and a.k5_mode == "fast":
         t += "f"
     return t
+
+
+def knn_mode():
+    """the K3 query pass the library selects (NAVGPU_KNN_MODE; 1 by default)"""
+    try:
+        return int(os.environ.get("NAVGPU_KNN_MODE", "1"))
+    except ValueError:
+        return 1
+
+
+def knn_query_kernel():
+    return "k_knng" if knn_mode() == 2 else "k_knnw"
+
+
+def load_trace(a, match):
+    """profiles/trace_k3.json (scripts/trace_check.py over the round's
+    rocprofv3 kernel trace of the default bench command) if its signature
+    matches `match`."""
+    if a.no_traffic_json:
+        return None
+    path = os.path.join(ROOT, "profiles", "trace_k3.json")
+    if not os.path.exists(path):
+        return None
+    with open(path) as f:
+        tj = json.load(f)
+    if not all(tj.get(k) == v for k, v in match.items()):
+        return None
+    tj.setdefault("source", os.path.relpath(path, ROOT))
+    return tj
 
 
 def load_traffic(a, match):

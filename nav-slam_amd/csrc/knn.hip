@@ -1443,6 +1443,18 @@ struct F3 {
 #define NAVGPU_ABL 0
 #endif
 constexpr int kAbl = NAVGPU_ABL;
+// non-temporal hints on the accesses nobody re-reads (r5 A/B knobs): the
+// random query-point lines and the result stores, so that they do not evict
+// the neighbourhood's records from the XCD's L2
+#ifndef NAVGPU_KNNG_NT_Q
+#define NAVGPU_KNNG_NT_Q 0
+#endif
+#ifndef NAVGPU_KNNG_NT_OUT
+#define NAVGPU_KNNG_NT_OUT 1  // (r5 bench A/B: 0.2544 against 0.2589 ms; NT_Q lost)
+#endif
+constexpr bool kNtQ = NAVGPU_KNNG_NT_Q, kNtOut = NAVGPU_KNNG_NT_OUT;
+typedef double d2v __attribute__((ext_vector_type(2)));
+typedef int i4v __attribute__((ext_vector_type(4)));
 
 template <int K>
 __global__ __launch_bounds__(kWave, NAVGPU_KNNG_MINW) void k_knng(
@@ -1490,7 +1502,9 @@ __global__ __launch_bounds__(kWave, NAVGPU_KNNG_MINW) void k_knng(
     gb = npg[row * (g0 + 1) + min(x + S + 1, g0)];
   }
   const double *qp = QS.pts + 3 * (size_t)qidx;
-  const double qv[3] = {qp[0], qp[1], qp[2]};
+  const double qv[3] = {kNtQ ? __builtin_nontemporal_load(qp) : qp[0],
+                        kNtQ ? __builtin_nontemporal_load(qp + 1) : qp[1],
+                        kNtQ ? __builtin_nontemporal_load(qp + 2) : qp[2]};
 #ifdef NAVGPU_STAMPS
   unsigned long long gst[8] = {__builtin_amdgcn_s_memrealtime(), 0, 0, 0, 0, 0, 0, 0};
 #endif
@@ -1780,14 +1794,26 @@ __global__ __launch_bounds__(kWave, NAVGPU_KNNG_MINW) void k_knng(
         const int qa = 16 * i + (lane >> 2), pc = lane & 3;
         const int q = rq[qa];
         const double2 v = *(const double2 *)(rd + qa * 8 + 2 * pc);
-        if (q >= 0) *(double2 *)(odist + (size_t)q * 8 + 2 * pc) = v;
+        if (q >= 0) {
+          double2 *o = (double2 *)(odist + (size_t)q * 8 + 2 * pc);
+          if (kNtOut)
+            __builtin_nontemporal_store(d2v{v.x, v.y}, (d2v *)o);
+          else
+            *o = v;
+        }
       }
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
         const int qa = 32 * i + (lane >> 1), pc = lane & 1;
         const int q = rq[qa];
         const int4 v = *(const int4 *)(ri + qa * 8 + 4 * pc);
-        if (q >= 0) *(int4 *)(oidx + (size_t)q * 8 + 4 * pc) = v;
+        if (q >= 0) {
+          int4 *o = (int4 *)(oidx + (size_t)q * 8 + 4 * pc);
+          if (kNtOut)
+            __builtin_nontemporal_store(i4v{v.x, v.y, v.z, v.w}, (i4v *)o);
+          else
+            *o = v;
+        }
       }
     }
     la = lb;

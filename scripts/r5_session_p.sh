@@ -1,0 +1,6 @@
+#!/bin/bash
+OUT=gpurun_out/$1; mkdir -p "$OUT"
+export PYTHONUNBUFFERED=1 NAVSLAM_QUIET=1
+NAVSLAM_HOST_TREES=0 NAVSLAM_PROFILE=1 timeout -k 10 300 python3 bench.py --workload k5 --k5-mode fast --steps 60 --warmup 5 --no-cpu-baseline --json-out "$OUT/k5_lazy.json" > "$OUT/k5_lazy.log" 2>&1 || { tail "$OUT/k5_lazy.log"; exit 1; }
+grep "navslam profile" "$OUT/k5_lazy.log"
+python3 -c "import json; d=json.load(open('$OUT/k5_lazy.json')); print(d['ms_per_step'], d['copy_floor_ms'], d['frac_of_copy_floor'], d['copy_floor'], d['kernel_us'])"

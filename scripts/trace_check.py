@@ -1,5 +1,5 @@
 """Cross-check of a K3 bench line against the rocprofv3 kernel trace of the
-same run: per launch of the query pass (k_knnw<K>, or k_knn<K>), the summed durations of the index build
+same run: per launch of the query pass (k_knnw<K> or k_knng<K>), the summed durations of the index build
 kernels, of the query-stage kernels and of the curvature, beside the line's
 HIP-event kernel_us (their span on the context's stream).
 
@@ -23,7 +23,15 @@ def per_launch(keys):
     return round(ns / max(launches, 1) / 1e3, 2)
 
 
+main = [r for r in rows if any(m in r["Name"] for m in QUERY_MAIN)]
 rec = {"launches": launches,
+       # the dominant kernel alone (bench.py quotes it as the trace basis of
+       # its roofline beside the HIP-event span)
+       "main_kernel": main[0]["Name"] if main else None,
+       "main_avg_us": (round(sum(float(r["TotalDurationNs"]) for r in main) / max(launches, 1) / 1e3, 2)
+                       if main else None),
+       "k": b["config"].get("k"), "points_per_cloud": b["config"].get("points_per_cloud"),
+       "knn_mode": b["config"].get("knn_mode"),
        "trace_us": {"knn_build": per_launch(BUILD_KERNELS),
                     "knn_query": per_launch(QUERY_KERNELS),
                     "curvature": per_launch(("k_curvature",))},
