@@ -118,6 +118,17 @@ static int adam_fast(void)
     return q && strcmp(q, "fast") == 0;
 }
 
+/* How the map slot comes back (NAVSLAM_D2H, r5 A/B knob): 0 (default) on
+ * the main stream after the trees build, 1 on the side stream while they
+ * build (r4). Both go through navgpu_download's 2-4 MB pieces. A page-locked
+ * bounce buffer was measured in r5 and lost: the host memcpy out of it runs
+ * at 22-31 GB/s against the DMA's 52 (profiles/r5/README.md). */
+static int side_d2h(void)
+{
+    const char *q = getenv("NAVSLAM_D2H");
+    return q && *q == '1';
+}
+
 static int host_trees(void)
 {
     const char *q = getenv("NAVSLAM_HOST_TREES");
@@ -410,7 +421,9 @@ static void map_frame(SLAM_attr *attr, slam_state *s, Pos pos,
     attr->globalPointCloud[slot].ToF_timestamps = lidar->ToF_timestamps;
     CK(navgpu_upload(c, s->d_lidar, &lidar->ToF_position[0][0], 24 * NPTS));
     CK(navgpu_transform_dev(c, s->d_lidar, NPTS, R, t, NULL, s->d_global, NULL));
-    CK(navgpu_side_mark(c)); /* the map slot is final here */
+    const int side = side_d2h();
+    if (side)
+        CK(navgpu_side_mark(c)); /* the map slot is final here */
     /* without host trees nobody walks a tree the next localisation does not
      * need: the rows keep their features in column order and only rows with
      * a distance tie get the reference's tree (navgpu_kd_query_rows_lazy_dev) */
@@ -421,9 +434,12 @@ static void map_frame(SLAM_attr *attr, slam_state *s, Pos pos,
     else
         CK(navgpu_kd_build_rows_dev(c, s->d_lidar, s->d_global, ROWS, COLS,
                                     s->d_tree, s->d_tcol, s->d_tn, NULL));
-    /* the map slot comes back while the trees build */
-    CK(navgpu_side_download(c, &attr->globalPointCloud[slot].ToF_position[0][0],
-                            s->d_global, 24 * NPTS));
+    if (side) /* the map slot comes back while the trees build */
+        CK(navgpu_side_download(c, &attr->globalPointCloud[slot].ToF_position[0][0],
+                                s->d_global, 24 * NPTS));
+    else
+        CK(navgpu_download(c, &attr->globalPointCloud[slot].ToF_position[0][0],
+                           s->d_global, 24 * NPTS));
     s->have_trees = 1;
     if (!host_trees()) {
         CK(navgpu_sync(c));

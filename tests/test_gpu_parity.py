@@ -968,6 +968,44 @@ def test_shim_l9_stream_vs_oracle(monkeypatch, R, Cc, F, steps, trees):
     assert attr.frameCount == s.frame_count
 
 
+@pytest.mark.parametrize("d2h,piece", [("0", "4096"), ("1", "4096"), ("0", "0"), ("0", "1000")])
+def test_shim_copy_paths_vs_oracle(monkeypatch, d2h, piece):
+    """Both ways the map slot comes back (NAVSLAM_D2H: 0 main stream, 1 side
+    stream) with navgpu_download's pieces (NAVGPU_D2H_PIECE_KB: 4096 -> two
+    3 MB pieces, 1000 -> seven with a short tail, 0 -> one copy) on the K5
+    loop at 128 x 2048: every map slot and pose bit-exact against the
+    oracle."""
+    monkeypatch.setenv("NAVGPU_D2H_PIECE_KB", piece)
+    monkeypatch.setenv("NAVSLAM_QUIET", "1")
+    monkeypatch.setenv("NAVSLAM_HOST_TREES", "0")
+    monkeypatch.setenv("NAVSLAM_D2H", d2h)
+    from pyoracle import Oracle, OracleSlam
+    from shimlib import Pos, Shim
+    from navslam.synth import l9_stream, l9_stream_index
+    R, Cc, F = 128, 2048, 3
+    frames = l9_stream(R, Cc, F, seed=23)
+    sh = Shim(R, Cc)
+    attr = sh.SLAMAttr()
+    pcs = [sh.cloud(f) for f in frames]
+    zero = np.zeros(6)
+    sh.L.init_slam(C.byref(attr), Pos.of(zero), C.byref(pcs[0]))
+    s = OracleSlam(Oracle(), R, Cc)
+    s.init(zero, frames[0])
+    slot = lambda n: np.frombuffer(bytes(attr.globalPointCloud[n % 100].pos),
+                                   np.float64).reshape(R, Cc, 3)
+    _eq(slot(0), s.last_global(), "map slot 0")
+    last_g, last_o = Pos.of(zero), zero
+    for i in range(1, 5):
+        f = l9_stream_index(i, F)
+        meas = sh.L.slam_localization(C.byref(attr), C.byref(pcs[f]), last_g, last_g)
+        sh.L.slam_mapping(C.byref(attr), meas, C.byref(pcs[f]))
+        om, _, _ = s.localization(frames[f], last_o, last_o)
+        s.mapping(om, frames[f])
+        _eq(np.array(meas.tolist()), om, f"frame {i} pose")
+        _eq(slot(attr.frameCount - 1), s.last_global(), f"map slot {i}")
+        last_g, last_o = meas, om
+
+
 @pytest.mark.parametrize("trees", ["1", "0"])
 def test_shim_localise_twice_between_mappings(monkeypatch, trees):
     """Two localisations against the same map (no slam_mapping between them,
