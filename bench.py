@@ -879,11 +879,13 @@ def traffic_tag(a):
 
 
 def knn_mode():
-    """the K3 query pass the library selects (NAVGPU_KNN_MODE; 1 by default)"""
+    """the K3 query pass the library selects (NAVGPU_KNN_MODE 1 or 2; anything
+    else keeps the default 2, as navgpu_create does)"""
     try:
-        return int(os.environ.get("NAVGPU_KNN_MODE", "1"))
+        m = int(os.environ.get("NAVGPU_KNN_MODE", "2"))
     except ValueError:
-        return 1
+        return 2
+    return m if m in (1, 2) else 2
 
 
 def knn_query_kernel():

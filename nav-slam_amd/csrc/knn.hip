@@ -1453,15 +1453,6 @@ constexpr int kAbl = NAVGPU_ABL;
 #define NAVGPU_KNNG_NT_OUT 1  // (r5 bench A/B: 0.2544 against 0.2589 ms; NT_Q lost)
 #endif
 constexpr bool kNtQ = NAVGPU_KNNG_NT_Q, kNtOut = NAVGPU_KNNG_NT_OUT;
-// chunks per wave (r5 A/B knob): kGCpw consecutive chunks of the pool
-#ifndef NAVGPU_KNNG_CPW
-#define NAVGPU_KNNG_CPW 1
-#endif
-constexpr int kGCpw = NAVGPU_KNNG_CPW;
-#ifndef NAVGPU_KNNG_PREB
-#define NAVGPU_KNNG_PREB 1  // the next chunk's block bounds prefetched too
-#endif
-constexpr bool kGPreB = NAVGPU_KNNG_PREB;
 typedef double d2v __attribute__((ext_vector_type(2)));
 typedef int i4v __attribute__((ext_vector_type(4)));
 
@@ -1489,9 +1480,8 @@ __global__ __launch_bounds__(kWave, NAVGPU_KNNG_MINW) void k_knng(
   const int per = (nchunk + 7) / 8;
   const int pool = (int)(blockIdx.x & 7);
   const int pend = min(nchunk, (pool + 1) * per);  // the pool's end
-  int chunk = pool * per + (int)(blockIdx.x >> 3) * kGCpw;
+  const int chunk = pool * per + (int)(blockIdx.x >> 3);
   if (chunk >= pend) return;
-  const int cend = min(chunk + kGCpw, pend);
   const int lane = (int)threadIdx.x;
   const uint32_t vmask = ~kKeyMask;
   int bad = 0;  // an index that had to be clamped (a logic error)
@@ -1500,27 +1490,19 @@ __global__ __launch_bounds__(kWave, NAVGPU_KNNG_MINW) void k_knng(
   // caller's cloud (issued after the bounds: only the scan needs it).
   // (Carrying the points through the build instead, so that a chunk reads 64
   // consecutive records, was measured in r5: the pass's raw FETCH 165 ->
-  // 105 MB and its time -3 us, the build +16-20 us.)
-  auto cells = [&](int c, int &cl, int &ix) {
-    const int qc = min(c * kWave + lane, nq - 1);
-    cl = QS.cell[qc];
-    ix = QS.idx[qc];
-  };
-  auto bounds = [&](int c, int cl, int &a, int &b) {
-    const bool lv = c * kWave + lane < nq;
-    const int row = lv ? cl / g0 : 0;
-    const int x = lv ? cl - row * g0 : 0;
-    a = npg[row * (g0 + 1) + max(x - S, 0)];
-    b = npg[row * (g0 + 1) + min(x + S + 1, g0)];
-  };
-  int qcell, qidx, ga, gb;
-  cells(chunk, qcell, qidx);
-  bounds(chunk, qcell, ga, gb);
-  // kGCpw > 1: the next chunk's cells load at this one's start, its block
-  // bounds after this one's scan, so that its staging can start at once
-  int ncell = 0, nidx = 0, nga = 0, ngb = 0;
-  for (;;) {
-  if (kGCpw > 1 && chunk + 1 < cend) cells(chunk + 1, ncell, nidx);
+  // 105 MB and its time -3 us, the build +16-20 us. So were 2 or 3
+  // consecutive chunks per wave, the next chunk's cells and bounds loaded
+  // during this one: 140 -> 155 and 161 us, the extra registers spilling.)
+  const int qc = min(chunk * kWave + lane, nq - 1);
+  const int qcell = QS.cell[qc], qidx = QS.idx[qc];
+  int ga, gb;
+  {
+    const bool lv = chunk * kWave + lane < nq;
+    const int row = lv ? qcell / g0 : 0;
+    const int x = lv ? qcell - row * g0 : 0;
+    ga = npg[row * (g0 + 1) + max(x - S, 0)];
+    gb = npg[row * (g0 + 1) + min(x + S + 1, g0)];
+  }
   const double *qp = QS.pts + 3 * (size_t)qidx;
   const double qv[3] = {kNtQ ? __builtin_nontemporal_load(qp) : qp[0],
                         kNtQ ? __builtin_nontemporal_load(qp + 1) : qp[1],
@@ -1701,7 +1683,6 @@ __global__ __launch_bounds__(kWave, NAVGPU_KNNG_MINW) void k_knng(
       }
       NV_GT(ts2);
       NV_GADD(5, ts1, ts2);
-      if (kGCpw > 1 && kGPreB && la == 0 && chunk + 1 < cend) bounds(chunk + 1, ncell, nga, ngb);
       bool ok = !overflow && Dq < 1e17;
       double ed[K];
       int ei[K];
@@ -1858,13 +1839,6 @@ __global__ __launch_bounds__(kWave, NAVGPU_KNNG_MINW) void k_knng(
 #pragma unroll
     for (int i = 0; i < 8; ++i) g_gstamps[chunk][i] = gst[i];
 #endif
-  if (kGCpw == 1 || ++chunk >= cend) break;
-  qcell = ncell;
-  qidx = nidx;
-  ga = nga;
-  gb = ngb;
-  if (!kGPreB) bounds(chunk, qcell, ga, gb);
-  }
   if (__any(bad) && lane == 0) atomicOr(L_.err, 1);
 }
 
@@ -2266,6 +2240,7 @@ static int knn_run(navgpu_ctx *ctx, const double *tgt, size_t nt, const double *
     CHECK_LAUNCH("k_bin_fine");
     if (mode == 2) {
       // tasks (64 columns of a row) <= 2 cap / 64 + rows; a few per wave
+      // (4096 workgroups, one task per wave: build -2 us, bench flat in r5)
       const unsigned nbl = std::min<unsigned>(1024, std::max<unsigned>(1, grid1d(2 * (size_t)cap, 64 * kNbWaves * 2)));
       hipLaunchKernelGGL(k_nb_fill, dim3(nbl), dim3(kWave * kNbWaves), 0, s, gp,
                          (const int *)tstart, npg, gl);
@@ -2287,7 +2262,7 @@ static int knn_run(navgpu_ctx *ctx, const double *tgt, size_t nt, const double *
   const int nchunk = (int)((nq + kWave - 1) / kWave);
   const dim3 gw(8 * (((nchunk + 7) / 8 + kWPB - 1) / kWPB)), bw(kWave * kWPB);
   const QSide QS{queries, qperm, qcell};
-  const dim3 gg(8 * (unsigned)(((nchunk + 7) / 8 + kGCpw - 1) / kGCpw));
+  const dim3 gg(8 * (unsigned)((nchunk + 7) / 8));
 #define KNN_CASE(KK)                                                                        \
   case KK:                                                                                  \
     if (mode == 2)                                                                          \

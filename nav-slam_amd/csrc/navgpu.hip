@@ -2880,7 +2880,10 @@ int navgpu_create(int device, void *stream, navgpu_ctx **out) {
   navgpu_ctx *c = new navgpu_ctx();
   c->device = device;
   if (const char *st = getenv("NAVGPU_KNN_STATS")) c->knn_stats = *st && *st != '0';
-  if (const char *o = getenv("NAVGPU_KNN_MODE")) c->knn_mode = std::min(std::max(atoi(o), 1), 2);
+  if (const char *o = getenv("NAVGPU_KNN_MODE")) {  // 1 or 2; anything else keeps the default
+    const int m = atoi(o);
+    if (m == 1 || m == 2) c->knn_mode = m;
+  }
   if (const char *o = getenv("NAVGPU_KNN_SX")) {
     const int v = atoi(o);
     if (v >= 1 && v <= kKnnMaxSx) c->knn_sx = v;

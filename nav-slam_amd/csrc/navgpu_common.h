@@ -225,7 +225,7 @@ struct navgpu_ctx {
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   double knn_occ = 5.0;  // target points per h^3 grid cell (NAVGPU_KNN_OCC)
   int knn_sx = 3;        // x cells per h (NAVGPU_KNN_SX; r4: 3 -> build -5 us, query same)
-  int knn_mode = 1;      // query pass: 1 = k_knnw, 2 = k_knng (row lists, r5) (NAVGPU_KNN_MODE)
+  int knn_mode = 2;      // query pass: 2 = k_knng (row lists, r5), 1 = k_knnw (NAVGPU_KNN_MODE)
   bool knn_stats = false;
   int screen_rows = 0, screen_S = 0;  // last screened rows_match call (tie diagnostic)
 };
