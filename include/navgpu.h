@@ -260,9 +260,7 @@ void navgpu_host_free(navgpu_ctx *ctx, void *hptr);
  * refuses (the range stays pageable and every copy still works) */
 int navgpu_host_register(navgpu_ctx *ctx, void *hptr, size_t bytes);
 void navgpu_host_unregister(navgpu_ctx *ctx, void *hptr);
-/* stream-ordered copies on the context's stream (host memory pageable; a
- * download goes in pieces of 2-4 MB, NAVGPU_D2H_PIECE_KB, the runtime's fast
- * pageable path at those sizes -- r5) */
+/* stream-ordered copies on the context's stream (host memory pageable) */
 int navgpu_upload(navgpu_ctx *ctx, void *dst_dev, const void *src_host,
                   size_t bytes);
 int navgpu_download(navgpu_ctx *ctx, void *dst_host, const void *src_dev,

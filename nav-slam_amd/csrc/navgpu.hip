@@ -2942,24 +2942,6 @@ int navgpu_set_stream(navgpu_ctx *ctx, void *stream) {
 
 void *navgpu_stream(navgpu_ctx *ctx) { return ctx ? (void *)ctx->stream : nullptr; }
 
-// A device->host copy into pageable memory, in balanced pieces of 2-4 MB
-// (NAVGPU_D2H_PIECE_KB, default 4096; 0 = one copy). r5 probe
-// (scripts/copy_probe.py, profiles/r5/README.md): 6.3 MB into calloc'd
-// (4 KB-page) memory took 0.42-0.66 ms as one hipMemcpyAsync, 0.133 ms as
-// 3-4 MB pieces, 0.45-0.59 ms as 0.5-1 MB pieces (the runtime picks its
-// pageable path by size); uploads are fastest whole (0.12 ms).
-static int download_pieces(void *dst, const void *src, size_t bytes, hipStream_t st) {
-  const char *e = getenv("NAVGPU_D2H_PIECE_KB");
-  const long kb = e ? atol(e) : 4096;
-  const size_t piece = kb > 0 ? (size_t)kb << 10 : (size_t)0;
-  const size_t n = piece ? (bytes + piece - 1) / piece : 1;
-  const size_t len = ((bytes + n - 1) / n + 4095) & ~(size_t)4095;  // >= piece / 2 when n > 1
-  for (size_t o = 0; o < bytes; o += len)
-    HIP_TRY(hipMemcpyAsync((char *)dst + o, (const char *)src + o, std::min(len, bytes - o),
-                           hipMemcpyDeviceToHost, st));
-  return NAVGPU_OK;
-}
-
 int navgpu_sync(navgpu_ctx *ctx) {
   ARG_CHECK(ctx);
   HIP_TRY(hipStreamSynchronize(ctx->stream));
@@ -2981,7 +2963,8 @@ int navgpu_side_download(navgpu_ctx *ctx, void *dst, const void *src, size_t byt
   ARG_CHECK(dst && src);
   RC(ensure_aux(ctx));
   HIP_TRY(hipStreamWaitEvent(ctx->aux, ctx->ev_fork, 0));
-  return download_pieces(dst, src, bytes, ctx->aux);
+  HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, ctx->aux));
+  return NAVGPU_OK;
 }
 
 int navgpu_rows_max_cols(void) {
@@ -3773,7 +3756,8 @@ int navgpu_download(navgpu_ctx *ctx, void *dst, const void *src, size_t bytes) {
   ARG_CHECK(ctx);
   if (!bytes) return NAVGPU_OK;
   ARG_CHECK(dst && src);
-  return download_pieces(dst, src, bytes, ctx->stream);
+  HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, ctx->stream));
+  return NAVGPU_OK;
 }
 
 }  // extern "C"

@@ -118,11 +118,12 @@ static int adam_fast(void)
     return q && strcmp(q, "fast") == 0;
 }
 
-/* How the map slot comes back (NAVSLAM_D2H, r5 A/B knob): 0 (default) on
- * the main stream after the trees build, 1 on the side stream while they
- * build (r4). Both go through navgpu_download's 2-4 MB pieces. A page-locked
- * bounce buffer was measured in r5 and lost: the host memcpy out of it runs
- * at 22-31 GB/s against the DMA's 52 (profiles/r5/README.md). */
+/* NAVSLAM_D2H=1: the map slot downloads on the side stream while the trees
+ * build (the r4 path; r5 A/B knob). Default: on the main stream after them
+ * (~14 us of compaction to overlap). Either is a pageable copy: the runtime
+ * locks the caller's pages per call, at a cost that varied from ~0.1 to
+ * ~0.45 ms per 6.3 MB slot across r5's boxes; page-locked bounce buffers
+ * and piecewise copies did not beat it. */
 static int side_d2h(void)
 {
     const char *q = getenv("NAVSLAM_D2H");

@@ -36,6 +36,8 @@ step trace_k3 600 rocprofv3 --kernel-trace --stats -d "$OUT/trace_k3" -o run --o
 # events time the same isolated kernels
 step trace_k3_iso 600 rocprofv3 --kernel-trace --stats -d "$OUT/trace_k3_iso" -o run --output-format csv -- python3 bench.py --inflight 1 --steps 20 --warmup 3 $Q --json-out "$OUT/bench_k3_iso_traced.json"
 step trace_check 60 python3 scripts/trace_check.py "$(find "$OUT/trace_k3_iso" -name "*kernel_stats.csv" | head -1)" "$OUT/bench_k3_iso_traced.json" "$OUT/trace_check_k3.json"
+# the bench lines below quote it (bench.py load_trace); commit it afterwards
+cp "$OUT/trace_check_k3.json" profiles/trace_k3.json
 fi
 pmc() {  # pmc <w> <traffic args> -- <bench args>
   local w=$1; shift

@@ -968,17 +968,15 @@ def test_shim_l9_stream_vs_oracle(monkeypatch, R, Cc, F, steps, trees):
     assert attr.frameCount == s.frame_count
 
 
-@pytest.mark.parametrize("d2h,piece", [("0", "4096"), ("1", "4096"), ("0", "0"), ("0", "1000")])
-def test_shim_copy_paths_vs_oracle(monkeypatch, d2h, piece):
-    """Both ways the map slot comes back (NAVSLAM_D2H: 0 main stream, 1 side
-    stream) with navgpu_download's pieces (NAVGPU_D2H_PIECE_KB: 4096 -> two
-    3 MB pieces, 1000 -> seven with a short tail, 0 -> one copy) on the K5
-    loop at 128 x 2048: every map slot and pose bit-exact against the
-    oracle."""
-    monkeypatch.setenv("NAVGPU_D2H_PIECE_KB", piece)
+@pytest.mark.parametrize("d2h", ["0", "1"])
+def test_shim_copy_paths_vs_oracle(monkeypatch, d2h):
+    """Both ways the map slot comes back (NAVSLAM_D2H: 0 on the main stream
+    after the row compaction, 1 on the side stream during it) on the K5 loop
+    at 128 x 2048 (6.3 MB per slot): every map slot and pose bit-exact
+    against the oracle."""
+    monkeypatch.setenv("NAVSLAM_D2H", d2h)
     monkeypatch.setenv("NAVSLAM_QUIET", "1")
     monkeypatch.setenv("NAVSLAM_HOST_TREES", "0")
-    monkeypatch.setenv("NAVSLAM_D2H", d2h)
     from pyoracle import Oracle, OracleSlam
     from shimlib import Pos, Shim
     from navslam.synth import l9_stream, l9_stream_index
