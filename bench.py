@@ -17,10 +17,10 @@ sets (the north star's batched case), and `--workload k5` the streaming
 L9 loop of src/main.c:361-431 (slam_localization + slam_mapping per frame)
 through the drop-in C ABI (libnavslam_128x2048.so), one step = one frame.
 
-K3 keeps two pairs in flight by default (--inflight): consecutive steps
-alternate over two library contexts, each with its own stream, workspace
+K3 keeps three pairs in flight by default (--inflight): consecutive steps
+alternate over three library contexts, each with its own stream, workspace
 and outputs, so one pair's memory-bound index build overlaps the previous
-pair's issue-bound query. Every step still processes one whole pair.
+pairs' latency-bound queries. Every step still processes one whole pair.
 
 Launch: python bench.py [--gpus N --steps K --warmup W]; for N > 1 under
 torch.distributed.run (one rank per GPU, RCCL).
@@ -65,11 +65,12 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--graph", action="store_true",
                    help="k3: capture one step into a hipGraph and replay it")
-    p.add_argument("--inflight", type=int, default=2,
+    p.add_argument("--inflight", type=int, default=3,
                    help="k3: pairs in flight -- consecutive steps alternate over this many "
                         "contexts (own stream, workspace and outputs each), so one pair's "
-                        "HBM-bound index build overlaps the previous pair's issue-bound "
-                        "query (measured: 1 -> 0.345 ms/pair, 2 -> 0.294, 3 -> 0.294); "
+                        "HBM-bound index build overlaps the previous pairs' latency-bound "
+                        "queries (r5, k_knng: 2 -> 0.241-0.245 ms/pair, 3 -> 0.233-0.238, "
+                        "4 -> 0.248-0.249; r1's kernels: 2 and 3 both 0.294); "
                         "--graph needs --inflight 1")
     p.add_argument("--cpu-reps", type=int, default=5,
                    help="CPU baseline: timed repetitions (median), after one untimed warm-up")
@@ -629,6 +630,13 @@ def main():
                      "integer_mm": bool(a.integer_mm), "tie_rows": tie_rows,
                      "rows_per_step": pairs * R}
 
+    # setup: every context of the pairs in flight allocates its workspace on
+    # its first call, so each makes one call here, whatever --warmup is
+    # (outside the warmup and timed steps; the rotation is restarted)
+    if a.workload == "k3" and nf > 1:
+        for _ in range(nf):
+            step()
+        turn[0] = 0
     # warmup (grows the workspace, JITs nothing)
     for _ in range(a.warmup):
         step()

@@ -2336,21 +2336,26 @@ int navgpu_pair_knn_dev(navgpu_ctx *ctx, const double *src, const double *tgt, i
   // One curvature launch over both clouds, on a side stream forked from and
   // joined back into the context's stream: it is f64-bound and independent
   // of the (latency-bound) index build and query, so the two overlap.
-  RC(ensure_aux(ctx));
-  HIP_TRY(hipEventRecord(ctx->ev_fork, ctx->stream));
-  HIP_TRY(hipStreamWaitEvent(ctx->aux, ctx->ev_fork, 0));
-  {
-    TimedRegion tr(ctx, "curvature", ctx->aux);
-    if (src_mask && tgt_mask)
-      RC(launch_curvature(src, src_mask, nullptr, tgt, tgt_mask, nullptr, R, C, ctx->aux));
-    else if (src_mask)
-      RC(launch_curvature(src, src_mask, nullptr, nullptr, nullptr, nullptr, R, C, ctx->aux));
-    else
-      RC(launch_curvature(tgt, tgt_mask, nullptr, nullptr, nullptr, nullptr, R, C, ctx->aux));
+  // (NAVGPU_PAIR_SIDE=0: on the context's stream, one stream per context.)
+  const bool side = ctx->pair_side;
+  if (side) {
+    RC(ensure_aux(ctx));
+    HIP_TRY(hipEventRecord(ctx->ev_fork, ctx->stream));
+    HIP_TRY(hipStreamWaitEvent(ctx->aux, ctx->ev_fork, 0));
   }
-  HIP_TRY(hipEventRecord(ctx->ev_join, ctx->aux));
+  hipStream_t cs = side ? ctx->aux : ctx->stream;
+  {
+    TimedRegion tr(ctx, "curvature", cs);
+    if (src_mask && tgt_mask)
+      RC(launch_curvature(src, src_mask, nullptr, tgt, tgt_mask, nullptr, R, C, cs));
+    else if (src_mask)
+      RC(launch_curvature(src, src_mask, nullptr, nullptr, nullptr, nullptr, R, C, cs));
+    else
+      RC(launch_curvature(tgt, tgt_mask, nullptr, nullptr, nullptr, nullptr, R, C, cs));
+  }
+  if (side) HIP_TRY(hipEventRecord(ctx->ev_join, ctx->aux));
   const int rc = knn_run(ctx, tgt, N, src, N, k, idx, dist);
-  HIP_TRY(hipStreamWaitEvent(ctx->stream, ctx->ev_join, 0));  // join before returning
+  if (side) HIP_TRY(hipStreamWaitEvent(ctx->stream, ctx->ev_join, 0));  // join before returning
   return rc;
 }
 

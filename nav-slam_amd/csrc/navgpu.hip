@@ -2880,6 +2880,7 @@ int navgpu_create(int device, void *stream, navgpu_ctx **out) {
   navgpu_ctx *c = new navgpu_ctx();
   c->device = device;
   if (const char *st = getenv("NAVGPU_KNN_STATS")) c->knn_stats = *st && *st != '0';
+  if (const char *o = getenv("NAVGPU_PAIR_SIDE")) c->pair_side = atoi(o) != 0;
   if (const char *o = getenv("NAVGPU_KNN_MODE")) {  // 1 or 2; anything else keeps the default
     const int m = atoi(o);
     if (m == 1 || m == 2) c->knn_mode = m;
