@@ -778,7 +778,8 @@ def main():
             b_ms, b_n = kt.get("knn_build", (0.0, 0))
             if b_n:
                 bld = {"kernels": ("k_bbox_partial + k_bin_hist (with the grid) + k_bin_colscan + "
-                                   "k_bin_scatter + k_bin_fine (both clouds binned)"),
+                                   "k_bin_scatter + k_bin_fine (both clouds binned)"
+                                   + (" + k_nb_fill (row lists)" if knn_mode() == 2 else "")),
                        "avg_us": round(1000.0 * b_ms / b_n, 2),
                        "bytes_model": "24 B/target read (SURVEY 8d); the query binning is extra",
                        "algorithmic_bytes": 24 * N, "traffic": build_traffic}

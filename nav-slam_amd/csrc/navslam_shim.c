@@ -118,16 +118,21 @@ static int adam_fast(void)
     return q && strcmp(q, "fast") == 0;
 }
 
-/* NAVSLAM_D2H=1: the map slot downloads on the side stream while the trees
- * build (the r4 path; r5 A/B knob). Default: on the main stream after them
- * (~14 us of compaction to overlap). Either is a pageable copy: the runtime
- * locks the caller's pages per call, at a cost that varied from ~0.1 to
- * ~0.45 ms per 6.3 MB slot across r5's boxes; page-locked bounce buffers
- * and piecewise copies did not beat it. */
+/* Where the map slot downloads (NAVSLAM_D2H=1 side stream, =0 main stream;
+ * r5 A/B knob). Default: on the side stream while the host trees build
+ * (k_rows_build, ~0.5 ms to overlap), on the main stream after the lazy
+ * rows' ~14 us compaction (the side stream's blit path started ~370 us
+ * late in r5's trace). Either is a pageable copy: the runtime locks the
+ * caller's pages per call, at a cost that varied from ~0.1 to ~0.45 ms per
+ * 6.3 MB slot across r5's boxes; page-locked bounce buffers and piecewise
+ * copies did not beat it. */
+static int host_trees(void);
 static int side_d2h(void)
 {
     const char *q = getenv("NAVSLAM_D2H");
-    return q && *q == '1';
+    if (q && (*q == '0' || *q == '1'))
+        return *q == '1';
+    return host_trees();
 }
 
 static int host_trees(void)

@@ -50,7 +50,11 @@ pmc() {  # pmc <w> <traffic args> -- <bench args>
   W=$(find "$OUT/pmc_write_$w" -name "*counter_collection.csv" | head -1)
   step traffic_$w 120 python3 scripts/traffic_json.py "$F" "$W" "$OUT/traffic_$w.json" "$TAG" --workload "$w" "${targs[@]}" --src "python3 bench.py $*"
 }
-if part k3; then pmc k3 -- --steps 20 --warmup 3; fi
+if part k3; then
+pmc k3 -- --steps 20 --warmup 3
+# the query pass's instruction mix, one pair at a time (its own --pmc run)
+step pmc_sq_k3 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_INSTS_LDS SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES -d "$OUT/pmc_sq_k3" -o run --output-format csv -- python3 bench.py --inflight 1 --steps 10 --warmup 2 $Q
+fi
 if part pmc; then
 pmc k2 --points 262144 --pairs 1 -- --workload k2 --steps 10
 pmc k2i --points 262144 --pairs 1 -- --workload k2 --integer-mm --steps 10
@@ -59,15 +63,17 @@ pmc k4i --points 262144 --pairs 256 -- --workload k4 --integer-mm --steps 2 --wa
 pmc k5f --points 262144 -- --workload k5 --k5-mode fast --steps 20 --warmup 2
 fi
 if part bench; then
-step bench_k3 600 python3 bench.py --traffic-json "$OUT/traffic_k3.json" --json-out "$OUT/bench_k3.json"
-step bench_k3_inflight1 300 python3 bench.py --inflight 1 --no-cpu-baseline --traffic-json "$OUT/traffic_k3.json" --json-out "$OUT/bench_k3_inflight1.json"
-step bench_k2 300 python3 bench.py --workload k2 --steps 10 --traffic-json "$OUT/traffic_k2.json" --json-out "$OUT/bench_k2.json"
-step bench_k2i 300 python3 bench.py --workload k2 --integer-mm --steps 10 --traffic-json "$OUT/traffic_k2i.json" --json-out "$OUT/bench_k2i.json"
-step bench_k4 400 python3 bench.py --workload k4 --steps 3 --warmup 1 --traffic-json "$OUT/traffic_k4.json" --json-out "$OUT/bench_k4.json"
-step bench_k4i 400 python3 bench.py --workload k4 --integer-mm --steps 3 --warmup 1 --traffic-json "$OUT/traffic_k4i.json" --json-out "$OUT/bench_k4i.json"
+# a traffic json made earlier in this session, else the committed one
+tj() { if [ -f "$OUT/traffic_$1.json" ]; then echo "$OUT/traffic_$1.json"; else echo "profiles/traffic_$1.json"; fi; }
+step bench_k3 600 python3 bench.py --traffic-json "$(tj k3)" --json-out "$OUT/bench_k3.json"
+step bench_k3_inflight1 300 python3 bench.py --inflight 1 --no-cpu-baseline --traffic-json "$(tj k3)" --json-out "$OUT/bench_k3_inflight1.json"
+step bench_k2 300 python3 bench.py --workload k2 --steps 10 --traffic-json "$(tj k2)" --json-out "$OUT/bench_k2.json"
+step bench_k2i 300 python3 bench.py --workload k2 --integer-mm --steps 10 --traffic-json "$(tj k2i)" --json-out "$OUT/bench_k2i.json"
+step bench_k4 400 python3 bench.py --workload k4 --steps 3 --warmup 1 --traffic-json "$(tj k4)" --json-out "$OUT/bench_k4.json"
+step bench_k4i 400 python3 bench.py --workload k4 --integer-mm --steps 3 --warmup 1 --traffic-json "$(tj k4i)" --json-out "$OUT/bench_k4i.json"
 step bench_k5 400 python3 bench.py --workload k5 --steps 30 --warmup 2 --json-out "$OUT/bench_k5.json"
-step bench_k5_fast 400 python3 bench.py --workload k5 --k5-mode fast --steps 30 --warmup 2 --traffic-json "$OUT/traffic_k5f.json" --json-out "$OUT/bench_k5_fast.json"
-NAVSLAM_HOST_TREES=0 step bench_k5_fast_lazy 400 python3 bench.py --workload k5 --k5-mode fast --steps 30 --warmup 2 --no-traffic-json --json-out "$OUT/bench_k5_fast_lazy.json"
+step bench_k5_fast 400 python3 bench.py --workload k5 --k5-mode fast --steps 30 --warmup 2 --traffic-json "$(tj k5f)" --json-out "$OUT/bench_k5_fast.json"
+NAVSLAM_HOST_TREES=0 step bench_k5_fast_lazy 400 python3 bench.py --workload k5 --k5-mode fast --steps 300 --warmup 10 --no-traffic-json --json-out "$OUT/bench_k5_fast_lazy.json"
 step trace_k5 400 rocprofv3 --kernel-trace --stats -d "$OUT/trace_k5" -o run --output-format csv -- python3 bench.py --workload k5 --k5-mode fast --steps 20 --warmup 2 --no-cpu-baseline --no-traffic-json
 fi
 echo done

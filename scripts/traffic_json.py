@@ -37,7 +37,7 @@ if a.workload == "k3":
            "query": q, "build": b, "k_knn_main": main,
            "kernels": {"query": list(TRAFFIC_SETS["k3"][0]),
                        "build": list(TRAFFIC_SETS["k3_build"][0])},
-           "per": "launch of the query pass k_knnw<K> / k_knn<K> (one per step)"}
+           "per": "launch of the query pass k_knng<K> / k_knnw<K> (one per step)"}
 else:
     key = "k5" if a.workload.startswith("k5") else "rows"
     kern, anchor = TRAFFIC_SETS[key]

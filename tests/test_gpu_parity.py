@@ -968,15 +968,15 @@ def test_shim_l9_stream_vs_oracle(monkeypatch, R, Cc, F, steps, trees):
     assert attr.frameCount == s.frame_count
 
 
-@pytest.mark.parametrize("d2h", ["0", "1"])
-def test_shim_copy_paths_vs_oracle(monkeypatch, d2h):
+@pytest.mark.parametrize("d2h,trees", [("0", "0"), ("1", "0"), ("0", "1"), ("1", "1")])
+def test_shim_copy_paths_vs_oracle(monkeypatch, d2h, trees):
     """Both ways the map slot comes back (NAVSLAM_D2H: 0 on the main stream
-    after the row compaction, 1 on the side stream during it) on the K5 loop
-    at 128 x 2048 (6.3 MB per slot): every map slot and pose bit-exact
-    against the oracle."""
+    after the row trees / compaction, 1 on the side stream during them), with
+    host trees and lazy rows, on the K5 loop at 128 x 2048 (6.3 MB per
+    slot): every map slot and pose bit-exact against the oracle."""
     monkeypatch.setenv("NAVSLAM_D2H", d2h)
     monkeypatch.setenv("NAVSLAM_QUIET", "1")
-    monkeypatch.setenv("NAVSLAM_HOST_TREES", "0")
+    monkeypatch.setenv("NAVSLAM_HOST_TREES", trees)
     from pyoracle import Oracle, OracleSlam
     from shimlib import Pos, Shim
     from navslam.synth import l9_stream, l9_stream_index
