@@ -786,37 +786,54 @@ struct CurvJob {
 // shared distances move between lanes by shuffles; no LDS, no barrier
 // (r3: 24.4 -> 18.2 us for both 1M-point clouds of a K3 pair, against a
 // 256-point LDS tile with two barriers).
-constexpr int kCurvSeg = kWave - 4;  // output columns per wave
+// (r5) Each wave takes kCurvU consecutive segments of its row and issues all
+// their loads, from clamped addresses, before any is used (one point per
+// lane in flight left the kernel latency-bound).
+constexpr int kCurvSeg = kWave - 4;  // output columns per segment
+#ifndef NAVGPU_CURV_U
+#define NAVGPU_CURV_U 4
+#endif
+constexpr int kCurvU = NAVGPU_CURV_U;  // segments per wave
 __global__ __launch_bounds__(kCurvTile) void k_curvature(CurvJob J, int R, int C) {
   const int z = blockIdx.z;
   const double *pts = J.pts[z];
   const int r = blockIdx.y;
   const int lane = threadIdx.x & (kWave - 1);
-  const int c0 = ((int)blockIdx.x * (kCurvTile / kWave) + (int)threadIdx.x / kWave) * kCurvSeg;
-  if (c0 >= C) return;  // wave-uniform
-  const int j = c0 - 2 + lane;  // this lane's column
+  const int wv = (int)blockIdx.x * (kCurvTile / kWave) + (int)threadIdx.x / kWave;
+  if (wv * kCurvU * kCurvSeg >= C) return;  // wave-uniform
   const size_t rowoff = (size_t)r * C;
-  double x = 0.0, y = 0.0, w = 0.0;
-  if (j >= 0 && j < C) {
-    const double *p = pts + 3 * (rowoff + j);
-    x = p[0];
-    y = p[1];
-    w = p[2];
+  double x[kCurvU], y[kCurvU], w[kCurvU];
+#pragma unroll
+  for (int u = 0; u < kCurvU; ++u) {
+    const int j = (wv * kCurvU + u) * kCurvSeg - 2 + lane;  // this lane's column
+    const double *p = pts + 3 * (rowoff + min(max(j, 0), C - 1));
+    x[u] = p[0];
+    y[u] = p[1];
+    w[u] = p[2];
   }
-  const double x1 = __shfl_down(x, 1), y1 = __shfl_down(y, 1), w1 = __shfl_down(w, 1);
-  const double x2 = __shfl_down(x, 2), y2 = __shfl_down(y, 2), w2 = __shfl_down(w, 2);
-  const double dA = ref_dist(x, y, w, x1, y1, w1);  // d(j, j+1)
-  const double dB = ref_dist(x, y, w, x2, y2, w2);  // d(j, j+2)
-  const double dAm = __shfl_up(dA, 1);              // d(j-1, j)
-  const double dBm = __shfl_up(dB, 2);              // d(j-2, j)
-  if (lane < 2 || lane >= kWave - 2 || j >= C) return;
-  double cv = 0.0;
-  if (j >= 2 && j < C - 2) cv = curvature_of(dBm, dAm, dA, dB);  // src/slam.c:16-58
-  J.mask[z][rowoff + j] = cv > 0.1 ? 1 : 0;
-  if (J.curv[z]) J.curv[z][rowoff + j] = cv;
+#pragma unroll
+  for (int u = 0; u < kCurvU; ++u) {
+    const int c0 = (wv * kCurvU + u) * kCurvSeg;
+    if (c0 >= C) break;  // wave-uniform
+    const int j = c0 - 2 + lane;
+    const bool in = j >= 0 && j < C;
+    const double xx = in ? x[u] : 0.0, yy = in ? y[u] : 0.0, ww = in ? w[u] : 0.0;
+    const double x1 = __shfl_down(xx, 1), y1 = __shfl_down(yy, 1), w1 = __shfl_down(ww, 1);
+    const double x2 = __shfl_down(xx, 2), y2 = __shfl_down(yy, 2), w2 = __shfl_down(ww, 2);
+    const double dA = ref_dist(xx, yy, ww, x1, y1, w1);  // d(j, j+1)
+    const double dB = ref_dist(xx, yy, ww, x2, y2, w2);  // d(j, j+2)
+    const double dAm = __shfl_up(dA, 1);                 // d(j-1, j)
+    const double dBm = __shfl_up(dB, 2);                 // d(j-2, j)
+    if (lane < 2 || lane >= kWave - 2 || j >= C) continue;
+    double cv = 0.0;
+    if (j >= 2 && j < C - 2) cv = curvature_of(dBm, dAm, dA, dB);  // src/slam.c:16-58
+    J.mask[z][rowoff + j] = cv > 0.1 ? 1 : 0;
+    if (J.curv[z]) J.curv[z][rowoff + j] = cv;
+  }
 }
 constexpr int curv_grid_x(int C) {
-  return ((C + kCurvSeg - 1) / kCurvSeg + kCurvTile / kWave - 1) / (kCurvTile / kWave);
+  return ((C + kCurvSeg * kCurvU - 1) / (kCurvSeg * kCurvU) + kCurvTile / kWave - 1) /
+         (kCurvTile / kWave);
 }
 
 // -------------------------------------------------------------- R2 kernel
