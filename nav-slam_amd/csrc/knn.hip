@@ -529,7 +529,8 @@ __global__ __launch_bounds__(256, kBuildMinW) void k_bin_scatter(BinJob J, const
 }
 
 // One bucket: count its points per cell (LDS), scan, write the cell starts,
-// then place every point (targets) or its bucketed position (queries).
+// then place every target (its PRec and SRec) or every query (its index in the
+// caller's cloud and its cell: qperm, qcell).
 // Queries of a bucket of at most kFineStage points (the usual case) are
 // staged: each output position gets its input slot in LDS (lslot) and the
 // positions are written in order, coalesced, instead of one scattered 4-B
