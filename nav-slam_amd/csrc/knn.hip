@@ -331,6 +331,15 @@ struct BinPt {
   double x, y, z;
   int idx, cell;
 };
+// k_knng's staged target record (r5): the f32 offset from the grid centre, 12 B
+// (the record's position comes from the row list)
+struct F3 {
+  float x, y, z;
+};
+#ifndef NAVGPU_KNNG_PACK
+#define NAVGPU_KNNG_PACK 1  // 0: k_knng stages from the 16-B SRec (r5 A/B knob)
+#endif
+constexpr bool kKnngPack = NAVGPU_KNNG_PACK;
 // a query's coarse-bucketed key (k_bin_scatter -> k_bin_fine)
 struct QKey {
   int cell, idx;
@@ -344,6 +353,7 @@ struct BinSide {
   QKey *key;     // queries: coarse-bucketed (cell, index) keys
   PRec *sorted;  // targets: cell-sorted records
   SRec *srec;    // targets: the same, as k_knnw stages them
+  F3 *frec;      // targets: the same, as k_knng stages them (instead of srec)
   int *perm;     // queries: cell-sorted position -> the caller's index
   int *qcell;    // queries: cell-sorted position -> cell
   int *rawcell;  // queries: the cell of each point in the caller's order
@@ -648,7 +658,10 @@ __global__ __launch_bounds__(kBinFineThreads, kBuildMinW) void k_bin_fine(BinJob
         const int row = e.cell / g0;
         t.cx = e.cell - row * g0;
         S.sorted[lo + j] = t;
-        S.srec[lo + j] = make_srec(G, J.sglobal, e.x, e.y, e.z, e.cell, lo + j);
+        if (S.frec)
+          S.frec[lo + j] = F3{(float)(e.x - G.c[0]), (float)(e.y - G.c[1]), (float)(e.z - G.c[2])};
+        else
+          S.srec[lo + j] = make_srec(G, J.sglobal, e.x, e.y, e.z, e.cell, lo + j);
       }
     }
     return;
@@ -667,7 +680,10 @@ __global__ __launch_bounds__(kBinFineThreads, kBuildMinW) void k_bin_fine(BinJob
       const int row = e.cell / g0;
       t.cx = e.cell - row * g0;
       S.sorted[pos] = t;
-      S.srec[pos] = make_srec(G, J.sglobal, e.x, e.y, e.z, e.cell, pos);
+      if (S.frec)
+        S.frec[pos] = F3{(float)(e.x - G.c[0]), (float)(e.y - G.c[1]), (float)(e.z - G.c[2])};
+      else
+        S.srec[pos] = make_srec(G, J.sglobal, e.x, e.y, e.z, e.cell, pos);
     }
   };
 #pragma unroll
@@ -1434,10 +1450,6 @@ __device__ unsigned long long g_gstamps[kGStampChunks][8];
 #define NV_GADD(i, a, b)
 #endif
 
-struct F3 {
-  float x, y, z;
-};
-
 // Timing-only ablations (-DNAVGPU_ABL=bits, scripts/build_variants.sh; never
 // the product build, the results are wrong): 1 the exact stage's record
 // gathers, 8 the staged records read from a 1024-record window (L2-resident,
@@ -1462,7 +1474,8 @@ typedef int i4v __attribute__((ext_vector_type(4)));
 template <int K>
 __global__ __launch_bounds__(kWave, NAVGPU_KNNG_MINW) void k_knng(
     const GridParams *__restrict__ gp, const int *__restrict__ npg, const int *__restrict__ gl,
-    int ngl, const PRec *__restrict__ tsort, const SRec *__restrict__ srec, const QSide QS,
+    int ngl, const PRec *__restrict__ tsort, const F3 *__restrict__ frec, int fstride,
+    const QSide QS,
     int nq, int ntg, int32_t *__restrict__ oidx, double *__restrict__ odist, KnnLists L_) {
   // the round's image: an XY plane (x0 x1 y0 y1 per pair of slots) and a ZG
   // plane (z0 z1 g0 g1, g = the cell-sorted position)
@@ -1586,7 +1599,9 @@ __global__ __launch_bounds__(kWave, NAVGPU_KNNG_MINW) void k_knng(
 #pragma unroll
       for (int u = 0; u < kGU; ++u) {
         bad |= (unsigned)gpos[u] >= (unsigned)ntg;
-        rec[u] = *(const F3 *)&srec[min(max((kAbl & 8) ? (gpos[u] & 1023) : gpos[u], 0), ntg - 1)];
+        rec[u] = *(const F3 *)((const float *)frec +
+                               (size_t)fstride *
+                                   min(max((kAbl & 8) ? (gpos[u] & 1023) : gpos[u], 0), ntg - 1));
       }
 #pragma unroll
       for (int u = 0; u < kGU; ++u) {
@@ -2202,8 +2217,12 @@ static int knn_run(navgpu_ctx *ctx, const double *tgt, size_t nt, const double *
   J.s[0].rawcell = nullptr;
   J.s[1].rawcell = qraw;
   J.s[0].sorted = tsort;
-  J.s[0].srec = srec;
+  // k_knng reads 12-B F3 records (kKnngPack) in the same buffer, k_knnw the SRec
+  const bool pack = mode == 2 && kKnngPack;
+  J.s[0].srec = pack ? nullptr : srec;
+  J.s[0].frec = pack ? (F3 *)srec : nullptr;
   J.s[1].srec = nullptr;
+  J.s[1].frec = nullptr;
   J.s[1].sorted = nullptr;
   J.s[0].perm = nullptr;
   J.s[1].perm = qperm;
@@ -2270,7 +2289,8 @@ static int knn_run(navgpu_ctx *ctx, const double *tgt, size_t nt, const double *
   case KK:                                                                                  \
     if (mode == 2)                                                                          \
       hipLaunchKernelGGL((k_knng<KK>), gg, dim3(kWave), 0, s, gp, (const int *)npg,         \
-                         (const int *)gl, (int)ngl, tsort, srec, QS, (int)nq, (int)nt, idx,  \
+                         (const int *)gl, (int)ngl, tsort, (const F3 *)srec,                \
+                         pack ? 3 : 4, QS, (int)nq, (int)nt, idx,                           \
                          dist, lists);                                                      \
     else                                                                                    \
       hipLaunchKernelGGL((k_knnw<KK>), gw, bw, 0, s, gp, tstart, tsort, srec, QS, (int)nq,      \
