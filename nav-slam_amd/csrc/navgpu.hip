@@ -1856,9 +1856,11 @@ __global__ __launch_bounds__(NT) void k_rows_screen32(
 __global__ __launch_bounds__(kRowsBuildBlock) void k_rows_build(
     const double *__restrict__ feat_src, const double *__restrict__ coords,
     int R, int C, double *__restrict__ tree_pts, int32_t *__restrict__ tree_col,
-    int32_t *__restrict__ tree_n, int32_t *__restrict__ mask_out, int build) {
+    int32_t *__restrict__ tree_n, int32_t *__restrict__ mask_out, int build,
+    int32_t *__restrict__ built) {
   const RowsLds L = rows_lds(C, kRowsBlock, false);
   const int r = blockIdx.x;
+  if (built && threadIdx.x == 0) built[r] = 0;  // the row is back in column order (r5: no memset)
   const size_t rowoff = (size_t)r * C;
   const int n = row_stage_and_build(feat_src, coords, r, C, L, mask_out, build != 0);
   const double *FC = (const double *)(smem + L.fc);
@@ -2150,9 +2152,12 @@ __global__ __launch_bounds__(kRowsBlock) void k_rows_retree(
     double *__restrict__ tree_pts, int32_t *__restrict__ tree_col,
     const int32_t *__restrict__ tree_n, const double *__restrict__ feat_src,
     const double *__restrict__ queries, int C, int32_t *__restrict__ nn_pos,
-    double *__restrict__ nn_dist, const int32_t *__restrict__ tie, int32_t *__restrict__ built) {
+    double *__restrict__ nn_dist, int32_t *__restrict__ tie, int32_t *__restrict__ built) {
   const int r = blockIdx.x;
-  if (!tie[r]) return;  // uniform (a built row's ties were walked by the screen)
+  const int tied = tie[r];
+  __syncthreads();  // every thread has read the flag before it is cleared
+  if (!tied) return;  // uniform (a built row's ties were walked by the screen)
+  if (threadIdx.x == 0) tie[r] = 0;  // zero again for the next call (no memset, r5)
   const RowsLds L = rows_lds(C, kRowsBlock, true);
   const size_t rowoff = (size_t)r * C;
   const int n = tree_n[r];
@@ -3177,13 +3182,15 @@ int navgpu_transform_dev(navgpu_ctx *ctx, const double *pts, size_t n,
 static int rows_build_launch(navgpu_ctx *ctx, const double *feat_src,
                              const double *coords, int R, int C,
                              double *tree_pts, int32_t *tree_col,
-                             int32_t *tree_n, int32_t *mask_out, int build) {
+                             int32_t *tree_n, int32_t *mask_out, int build,
+                             int32_t *built = nullptr) {
   ARG_CHECK(ctx);
   RC(check_rows_shape(R, C, false));
   if (R == 0) return NAVGPU_OK;
   ARG_CHECK(tree_n);
   if (C == 0) {
     HIP_TRY(hipMemsetAsync(tree_n, 0, 4 * (size_t)R, ctx->stream));
+    if (built) HIP_TRY(hipMemsetAsync(built, 0, 4 * (size_t)R, ctx->stream));
     return NAVGPU_OK;
   }
   ARG_CHECK(feat_src && coords && tree_pts && tree_col);
@@ -3192,7 +3199,7 @@ static int rows_build_launch(navgpu_ctx *ctx, const double *feat_src,
   TimedRegion tr(ctx, "rows_build");
   hipLaunchKernelGGL(k_rows_build, dim3(R), dim3(kRowsBuildBlock), L.total,
                      ctx->stream, feat_src, coords, R, C, tree_pts, tree_col,
-                     tree_n, mask_out, build);
+                     tree_n, mask_out, build, built);
   CHECK_LAUNCH("k_rows_build");
   return NAVGPU_OK;
 }
@@ -3209,9 +3216,9 @@ int navgpu_kd_compact_rows_dev(navgpu_ctx *ctx, const double *feat_src,
                                double *tree_pts, int32_t *tree_col,
                                int32_t *tree_n, int32_t *mask_out, int32_t *tree_built) {
   ARG_CHECK(ctx && R >= 0);
-  if (tree_built && R > 0)  // every row back in column order
-    HIP_TRY(hipMemsetAsync(tree_built, 0, 4 * (size_t)R, ctx->stream));
-  return rows_build_launch(ctx, feat_src, coords, R, C, tree_pts, tree_col, tree_n, mask_out, 0);
+  // every row back in column order: k_rows_build zeroes tree_built[r]
+  return rows_build_launch(ctx, feat_src, coords, R, C, tree_pts, tree_col, tree_n, mask_out, 0,
+                           tree_built);
 }
 
 int navgpu_kd_rows_nodes_dev(navgpu_ctx *ctx, const double *tree_pts,
@@ -3349,8 +3356,12 @@ int navgpu_kd_query_rows_lazy_dev(navgpu_ctx *ctx, double *tree_pts, int32_t *tr
   if ((size_t)R * C == 0) return NAVGPU_OK;
   ARG_CHECK(tree_col);
   int32_t *tie;
-  RC(ws(ctx, kRowTie, (size_t)R, &tie));
-  HIP_TRY(hipMemsetAsync(tie, 0, 4 * (size_t)R, ctx->stream));
+  RC(ws(ctx, kRowTieLazy, (size_t)R, &tie));
+  if (tie != ctx->lazy_tie || R > ctx->lazy_tie_rows) {  // a new buffer: zero it once
+    HIP_TRY(hipMemsetAsync(tie, 0, 4 * (size_t)R, ctx->stream));
+    ctx->lazy_tie = tie;
+    ctx->lazy_tie_rows = R;
+  }
   RC(rows_query_launch(ctx, tree_pts, tree_n, feat_src, queries, R, C, nn_pos, nn_dist,
                        mask_out, tie, tree_col, tree_built));
   const RowsLds L = rows_lds(C, kRowsBlock, true);
@@ -3363,7 +3374,7 @@ int navgpu_kd_query_rows_lazy_dev(navgpu_ctx *ctx, double *tree_pts, int32_t *tr
   TimedRegion tr(ctx, "rows_retree");
   hipLaunchKernelGGL(k_rows_retree, dim3(R), dim3(kRowsBlock), L.total, ctx->stream, tree_pts,
                      tree_col, tree_n, feat_src, queries, C, nn_pos, nn_dist,
-                     (const int32_t *)tie, tree_built);
+                     tie, tree_built);
   CHECK_LAUNCH("k_rows_retree");
   return NAVGPU_OK;
 }

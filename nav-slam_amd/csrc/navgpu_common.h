@@ -227,7 +227,11 @@ struct navgpu_ctx {
   int knn_sx = 3;        // x cells per h (NAVGPU_KNN_SX; r4: 3 -> build -5 us, query same)
   int knn_mode = 2;      // query pass: 2 = k_knng (row lists, r5), 1 = k_knnw (NAVGPU_KNN_MODE)
   bool knn_stats = false;
-  bool pair_side = true;  // pair curvature on the side stream (NAVGPU_PAIR_SIDE=0: on this one)
+  bool pair_side = true;
+  // the lazy K5 query's tie flags (kRowTieLazy): zeroed once, then cleared by
+  // k_rows_retree as it reads them, so no memset per call
+  int32_t *lazy_tie = nullptr;
+  int lazy_tie_rows = 0;  // pair curvature on the side stream (NAVGPU_PAIR_SIDE=0: on this one)
   int screen_rows = 0, screen_S = 0;  // last screened rows_match call (tie diagnostic)
 };
 
@@ -238,7 +242,7 @@ enum Slot {
   kBBox = 1, kParams, kCnt, kStart, kBSum, kCellId, kSlotBuf, kRec, kTan,
   kKdFc, kKdP, kKdT, kQStart, kQCell, kQSlot, kQPerm, kStats, kOvf, kSlowQ,
   kSlowThr, kTSort, kRowMaskS, kRowMaskT, kRowTie, kCorrEnt, kCorrN, kCorrSums, kKdPtmp, kKdSel,
-  kQSort, kCellId2, kSRec, kNpg, kGl,
+  kQSort, kCellId2, kSRec, kNpg, kGl, kRowTieLazy,
   kH0 = 100, kH1, kH2, kH3, kH4, kH5,
 };
 

@@ -61,7 +61,9 @@ class Shim:
 
     def __init__(self, R, Cc):
         self.R, self.C = R, Cc
-        self.path = os.path.join(LIBDIR, f"libnavslam_{R}x{Cc}.so")
+        # NAVSLAM_LIBDIR: another build of the shim + libnavgpu (A/B runs only)
+        self.path = os.path.join(os.environ.get("NAVSLAM_LIBDIR") or LIBDIR,
+                                 f"libnavslam_{R}x{Cc}.so")
         from navslam.gpu import load_library
         load_library()  # libnavgpu bound to the process's (torch's) HIP runtime
         L = self.L = C.CDLL(self.path)
