@@ -72,6 +72,9 @@ def parse():
                         "queries (r5, k_knng: 2 -> 0.241-0.245 ms/pair, 3 -> 0.233-0.238, "
                         "4 -> 0.248-0.249; r1's kernels: 2 and 3 both 0.294); "
                         "--graph needs --inflight 1")
+    p.add_argument("--no-events", action="store_true",
+                   help="A/B diagnostic: no HIP timing events in the timed region (the line "
+                        "then has no kernel times or roofline)")
     p.add_argument("--cpu-reps", type=int, default=5,
                    help="CPU baseline: timed repetitions (median), after one untimed warm-up")
     p.add_argument("--resident-pairs", type=int, default=9,
@@ -292,8 +295,14 @@ def run_k5(a, ws, rank, dev):
     sh.L.init_slam(attr, zero, pcs[0])
     poses, state = [], {"i": 0, "last": zero, "q": 0}
 
+    # kernel timing (HIP events) on every 4th frame of the timed region only:
+    # events on every frame cost the frame ~4 % (r5)
+    ev = {"ctx": None, "L": None, "on": False}
+
     def frame():
         state["i"] += 1
+        if ev["on"]:
+            ev["L"].navgpu_timing_enable(ev["ctx"], 1 if state["i"] % 4 == 0 else 0)
         pc = pcs[synth.l9_stream_index(state["i"], F)]
         last = state["last"]
         meas = sh.L.slam_localization(attr, pc, last, last)
@@ -310,7 +319,7 @@ def run_k5(a, ws, rank, dev):
     ctx = sh.context()
     from navslam.gpu import load_library
     L = load_library()
-    L.navgpu_timing_enable(ctx, 1)
+    ev.update(ctx=ctx, L=L, on=not a.no_events)
     names = ["rows_build", "rows_query", "rows_retree"] + (["rows_corr"] if a.k5_mode == "fast" else [])
     for n in names:
         L.navgpu_timing_read(ctx, n.encode(), 1)
@@ -325,6 +334,7 @@ def run_k5(a, ws, rank, dev):
     if ws > 1:
         dist.barrier()
     t1 = time.perf_counter()
+    ev["on"] = False
     L.navgpu_timing_enable(ctx, 0)
     kt = {}
     for n in names:
@@ -645,12 +655,18 @@ def main():
         dist.barrier()
     # kernel timing on every context; each kernel's average is its summed
     # time over its own launch count (with pairs in flight, a context runs
-    # only every nf-th step)
+    # only every nf-th step). With pairs in flight the timed region records
+    # only the dominant query stage: events around every region of every
+    # step cost the K3 step ~2 % (r5: 0.2443 vs 0.2386 ms with no events,
+    # three interleaved rounds); the build and curvature come from the
+    # isolated steps after it
     names = sorted(set(path_kernels + [dom] + (["knn_build"] if a.workload == "k3" else [])))
+    only_dom = a.workload == "k3" and nf > 1
 
     def timing_on(on):
         for c in ctxs:
             c.timing(on)
+            c.timing_select(dom if (on and only_dom) else None)
             for name in names:
                 c.timing_read(name, reset=True)
 
@@ -660,11 +676,12 @@ def main():
             ms = n = 0
             for c in ctxs:
                 m_, n_ = c.timing_read(name, reset=True)
-                ms += m_
-                n += n_
+                if n_ > 0 and m_ >= 0:  # (-1 ms: the region was never recorded here)
+                    ms += m_
+                    n += n_
             agg[name] = (ms, n)
         return agg
-    timing_on(True)
+    timing_on(not a.no_events)
     torch.cuda.synchronize()
     if ws > 1:
         dist.barrier()
@@ -682,6 +699,7 @@ def main():
     # the timed region (K3 with pairs in flight only)
     kt_iso = None
     if iso_step is not None and nf > 1 and a.iso_steps > 0:
+        g.timing_select(None)  # every region of the isolated steps
         for _ in range(a.iso_steps):
             iso_step()
         torch.cuda.synchronize()
@@ -755,9 +773,10 @@ def main():
                     "kernel": ("query stage %s<%d> + k_knn_slow<%d>, one launch each per "
                                "step" % (knn_query_kernel(), a.k, a.k)),
                     "avg_us": round(dom_avg_us, 2), "launches": dom_n,
-                    "timing": ("HIP events on each context's stream over the timed region"
-                               + (f" ({nf} pairs in flight: a contended span that also holds "
-                                  "the other pair's interleaved kernels)" if nf > 1 else "")),
+                    "timing": ("HIP events on the context's stream over the timed region"
+                               + (f" ({nf} pairs in flight: context 0's launches only, a "
+                                  "contended span that also holds the other pairs' "
+                                  "interleaved kernels)" if nf > 1 else "")),
                     "bytes_per_launch": dom_bytes,
                     "bytes_model": "24 B/query read + 24 B/target read + 12*k B/query out"}
             tr = load_trace(a, {"k": a.k, "points_per_cloud": N, "knn_mode": knn_mode()})
@@ -776,11 +795,13 @@ def main():
             # headline fraction: its time, the 24 B/target read of the model
             # and its measured traffic
             b_ms, b_n = kt.get("knn_build", (0.0, 0))
-            if b_n:
+            b_iso_n = kt_iso.get("knn_build", (0, 0))[1] if kt_iso is not None else 0
+            if b_n or b_iso_n:
                 bld = {"kernels": ("k_bbox_partial + k_bin_hist (with the grid) + k_bin_colscan + "
                                    "k_bin_scatter + k_bin_fine (both clouds binned)"
                                    + (" + k_nb_fill (row lists)" if knn_mode() == 2 else "")),
-                       "avg_us": round(1000.0 * b_ms / b_n, 2),
+                       # (not timed in the timed region with pairs in flight)
+                       "avg_us": round(1000.0 * b_ms / b_n, 2) if b_n else None,
                        "bytes_model": "24 B/target read (SURVEY 8d); the query binning is extra",
                        "algorithmic_bytes": 24 * N, "traffic": build_traffic}
                 if kt_iso is not None and kt_iso.get("knn_build", (0, 0))[1] > 0:
@@ -842,7 +863,8 @@ def main():
                "config": dict({"workload": workload, "parallelism": f"replicas x{ws}"},
                               **cfg_extra),
                "roofline": roof, "curvature_plus_query": path,
-               "kernel_us": {k: round(1000.0 * v[0] / max(v[1], 1), 2) for k, v in kt.items()},
+               "kernel_us": {k: (round(1000.0 * v[0] / v[1], 2) if v[1] else None)
+                             for k, v in kt.items()},
                "kernel_us_isolated": (None if kt_iso is None else
                                       {k: round(1000.0 * v[0] / max(v[1], 1), 2)
                                        for k, v in kt_iso.items()}),

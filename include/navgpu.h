@@ -285,6 +285,10 @@ int navgpu_side_download(navgpu_ctx *ctx, void *dst_host, const void *src_dev,
  * the summed milliseconds of the named kernel since the last reset
  * (name: "knn_query", "rows_match", "curvature"), or -1. */
 void navgpu_timing_enable(navgpu_ctx *ctx, int on);
+/* Record only the region `name` while timing is on (NULL or "" = every
+ * region): fewer event packets in a measured run (r5: events around every
+ * region of every K3 step cost the step ~2 %). */
+void navgpu_timing_select(navgpu_ctx *ctx, const char *name);
 double navgpu_timing_read(navgpu_ctx *ctx, const char *name, int reset);
 int navgpu_timing_count(navgpu_ctx *ctx, const char *name);
 /* Diagnostic: queries of the last navgpu_knn_* call that left the fast path

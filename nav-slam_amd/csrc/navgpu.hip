@@ -3007,6 +3007,10 @@ void navgpu_timing_enable(navgpu_ctx *ctx, int on) {
   if (ctx) ctx->timing = on != 0;
 }
 
+void navgpu_timing_select(navgpu_ctx *ctx, const char *name) {
+  if (ctx) ctx->timing_only = name ? name : "";
+}
+
 double navgpu_timing_read(navgpu_ctx *ctx, const char *name, int reset) {
   if (!ctx || !name) return -1.0;
   auto it = ctx->ev.find(name);
@@ -3297,10 +3301,13 @@ static int rows_query_launch(navgpu_ctx *ctx, const double *tree_pts,
   ARG_CHECK(tree_pts && tree_n && feat_src && queries && nn_pos && nn_dist);
   const char *qt = getenv("NAVGPU_ROWS_QUERY_TREE");
   if (tie || !(qt && *qt && *qt != '0')) {
-    // the screen (default): >= 1024 workgroups, >= 128 columns each (two
-    // ~74 KB workgroups per CU at C = 2048)
+    // the screen (default): >= 512 workgroups, >= 128 columns each (two
+    // ~74 KB workgroups per CU at C = 2048; r5: 128 x 2048 frames 107 -> 103
+    // us against >= 1024)
     int S = 1;
-    while (S < 16 && (long long)R * S < 1024 && C / (2 * S) >= 128) S <<= 1;
+    while (S < 16 && (long long)R * S < 512 && C / (2 * S) >= 128) S <<= 1;
+    if (const char *e = getenv("NAVGPU_ROWSQ_S"); e && *e)  // A/B: column splits per row
+      S = std::max(1, std::min(64, atoi(e)));
     const int w = (C + S - 1) / S;
     const int cp = (C + kScreenChunk - 1) / kScreenChunk * kScreenChunk;
     // (the last region: the walk stacks, or the lazy rows' feature columns)

@@ -217,6 +217,7 @@ struct navgpu_ctx {
   bool own_stream = false;
   std::map<int, std::pair<void *, size_t>> bufs;  // grow-only workspace
   bool timing = false;
+  std::string timing_only;  // navgpu_timing_select: record only this region ("" = all)
   std::map<std::string, std::vector<std::pair<hipEvent_t, hipEvent_t>>> ev;
   std::vector<hipEvent_t> free_ev;
   std::vector<double> tan_c, tan_r;
@@ -274,13 +275,13 @@ struct TimedRegion {
   }
   TimedRegion(navgpu_ctx *c, const char *n, hipStream_t on = nullptr)
       : ctx(c), name(n), st(on ? on : c->stream) {
-    if (!ctx->timing) return;
+    if (!ctx->timing || (!ctx->timing_only.empty() && ctx->timing_only != name)) return;
     a = take();
     b = take();
     if (a && b) (void)hipEventRecord(a, st);
   }
   ~TimedRegion() {
-    if (!ctx->timing || !a || !b) return;
+    if (!a || !b) return;
     (void)hipEventRecord(b, st);
     ctx->ev[name].push_back({a, b});
   }

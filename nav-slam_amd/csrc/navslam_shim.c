@@ -340,6 +340,7 @@ typedef struct {
     SLAM_attr *key;
     double *d_lidar, *d_global, *d_last, *d_tree, *d_dist, *d_sums, *d_list;
     double h_sums[6 * ROWS];
+    double *h_sums_pin; /* page-locked, written by k_rows_corr itself (r5), or NULL */
     int32_t *d_tcol, *d_tn, *d_pos, *d_count;
     int32_t *d_built; /* lazy rows already turned into the reference tree */
     int have_trees;
@@ -393,6 +394,10 @@ static slam_state *state_for(SLAM_attr *a)
         abort();
     }
     register_slab(s->h_nodes, NPTS);
+    /* the fast mode's per-row sums land here straight from the kernel: no
+     * copy launch per frame (NULL when page-locked memory is refused) */
+    if (navgpu_host_alloc(c, sizeof(s->h_sums), (void **)&s->h_sums_pin) != 0)
+        s->h_sums_pin = NULL;
     g_states = realloc(g_states, sizeof(*g_states) * (g_nstates + 1));
     g_states[g_nstates++] = s;
     return s;
@@ -510,15 +515,17 @@ static Pos localization_fast(SLAM_attr *attr, slam_state *s, double transform[6]
 {
     navgpu_ctx *c = ctx();
     CK(navgpu_rows_corr_dev(c, s->d_tree, s->d_tn, s->d_pos, s->d_dist, s->d_global,
-                            ROWS, COLS, NULL, s->d_sums));
-    CK(navgpu_download(c, s->h_sums, s->d_sums, sizeof(s->h_sums)));
+                            ROWS, COLS, NULL, s->h_sums_pin ? s->h_sums_pin : s->d_sums));
+    if (!s->h_sums_pin)
+        CK(navgpu_download(c, s->h_sums, s->d_sums, sizeof(s->h_sums)));
     CK(navgpu_sync(c));
+    const double *sums = s->h_sums_pin ? s->h_sums_pin : s->h_sums;
     PROF_ADD(2, s->prof_t0);
     /* merge the rows' (count, mean, centred M2) with Chan et al.'s pairwise
      * update: M2 = M2a + M2b + |mb - ma|^2 na nb / (na + nb) */
     double mean[3] = {0.0, 0.0, 0.0}, M2 = 0.0, n = 0.0, nq = 0.0;
     for (int r = 0; r < ROWS; r++) {
-        const double *h = s->h_sums + 6 * r;
+        const double *h = sums + 6 * r;
         nq += h[5];
         const double nb = h[4];
         if (!(nb > 0))

@@ -79,6 +79,7 @@ def _declare(L):
         "navgpu_side_mark": (C.c_int, [_vp]),
         "navgpu_side_download": (C.c_int, [_vp, _vp, _vp, _sz]),
         "navgpu_timing_enable": (None, [_vp, C.c_int]),
+        "navgpu_timing_select": (None, [_vp, C.c_char_p]),
         "navgpu_timing_read": (C.c_double, [_vp, C.c_char_p, C.c_int]),
         "navgpu_timing_count": (C.c_int, [_vp, C.c_char_p]),
         "navgpu_knn_fallbacks": (C.c_longlong, [_vp]),
@@ -170,6 +171,10 @@ class NavGpu:
 
     def timing(self, on=True):
         self.L.navgpu_timing_enable(self.h, 1 if on else 0)
+
+    def timing_select(self, name=None):
+        """Record only the region `name` while timing is on (None: all)."""
+        self.L.navgpu_timing_select(self.h, None if name is None else name.encode())
 
     def stream_copy_dev(self, dst, src, nbytes):
         """Device-to-device copy by a plain streaming kernel (the measured HBM
