@@ -1,5 +1,5 @@
 #!/bin/bash
-# K5 frames without the per-frame memsets (tie flags cleared by k_rows_retree,
+# K5 A/B of the shim at HEAD (variants/old) against the working tree
 # built flags by k_rows_build): lazy-row tests, then 300-frame A/B against HEAD's build
 OUT=gpurun_out/$1; mkdir -p "$OUT"
 export PYTHONUNBUFFERED=1 NAVSLAM_QUIET=1
