@@ -551,7 +551,7 @@ constexpr int kLaneSubtree = NAVGPU_LANE_SUBTREE;  // subarrays this short: one 
 #endif
 constexpr int kBlockNthMin = NAVGPU_BLOCK_NTH_MIN;  // root partition by the block from here
 #ifndef NAVGPU_BLOCK_LEVEL_MIN
-#define NAVGPU_BLOCK_LEVEL_MIN 512
+#define NAVGPU_BLOCK_LEVEL_MIN 1024  // (r5: 512 -> 1024, K2i 0.728 -> 0.715 ms, K4i flat)
 #endif
 constexpr int kBlockLevelMin = NAVGPU_BLOCK_LEVEL_MIN;  // deeper levels by the block from here
 
