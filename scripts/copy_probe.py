@@ -1,7 +1,11 @@
 """PCIe copy probe for the K5 frame (r5): per-call times of the frame's
 6.3 MB host<->device copies, with the host side (a) one fixed buffer,
 (b) rotating over 8 source clouds / 100 map slots as the K5 loop does,
-(c) a page-locked buffer, and (d) a host memcpy of the same size.
+(c) a page-locked buffer, (d) a host memcpy of the same size, and (e)
+pageable downloads into calloc'd slots whole and in pieces of 0.5-5 MB
+(issued here as separate navgpu_download calls). The page-locked
+bounce-buffer path it also timed in r5 was removed from the library after
+losing (profiles/r5/copy_probe_staged.json).
 Prints one JSON line. GPU only."""
 import ctypes as C
 import json
@@ -76,16 +80,6 @@ def main():
         timeit(f"d2h_crot100_{kb}k", dl_chunks)
         timeit(f"h2d_crot8_{kb}k", ul_chunks)
 
-    def staged_dl(i):
-        L.navgpu_download_staged(h2, slots[(7 * i) % 100].ctypes.data, d, nb)
-
-    for kb in ():
-        os.environ["NAVGPU_STAGE_KB"] = str(kb)
-        g2 = NavGpu()
-        h2 = g2.h
-        timeit(f"d2h_staged_{kb}k", staged_dl)
-        timeit(f"h2d_staged_{kb}k", lambda i: L.navgpu_upload_staged(h2, d, src[i % 8].ctypes.data, nb))
-        g2.close()
     print(json.dumps(out), flush=True)
 
 

@@ -1,7 +1,9 @@
 """K5 mapping-call sequence probe (r5): per-call host time of
 upload(cloud) -> transform -> download(map slot) with calloc'd (4 KB-page)
 host buffers as the K5 caller has them, in variants that separate where the
-time goes. Prints one JSON line. GPU only."""
+time goes, and a page-locked stage copied out by 1-8 host threads (the
+bounce path DESIGN.md §4 r5 measured and dropped). Prints one JSON line.
+GPU only."""
 import ctypes as C
 import json
 import os
@@ -66,10 +68,6 @@ def main():
     run("up_tf_down", [up, tf, down])
     run("up_tf_sync_down", [up, tf, sync, down])
     run("up_sync_tf_sync_down", [up, sync, tf, sync, down])
-    os.environ["NAVGPU_D2H_PIECE_KB"] = "0"
-    run("down_whole", [down])
-    run("up_tf_down_whole", [up, tf, down])
-    run("up_tf_sync_down_whole", [up, tf, sync, down])
     # page-locked stage + parallel host copy-out (ctypes.memmove drops the GIL)
     from concurrent.futures import ThreadPoolExecutor
     pin = C.c_void_p()
