@@ -77,21 +77,28 @@ constexpr uint32_t kNoKey = 0xffffffffu;
 
 constexpr int kBBoxBlocks = 256;  // bbox partials (every k_bin_hist block reduces them)
 
+#ifndef NAVGPU_BBOX_U
+#define NAVGPU_BBOX_U 4
+#endif
 // per-block min/max of the finite coordinates -> part[block][6]
 __global__ __launch_bounds__(256) void k_bbox_partial(const double *__restrict__ p,
                                                       size_t n, double *__restrict__ part) {
   __shared__ double s[4][6];
   double v6[6] = {INFINITY, INFINITY, INFINITY, -INFINITY, -INFINITY, -INFINITY};
-  // batches of 4 points per thread, all loads of a batch in flight together
-  constexpr int U = 4;
+  // batches of U points per thread, all loads of a batch in flight together,
+  // issued unconditionally from clamped indices (r5: a conditional load per
+  // element makes hipcc branch and wait around each)
+  constexpr int U = NAVGPU_BBOX_U;
   const size_t stride = (size_t)gridDim.x * blockDim.x;
   for (size_t ib = (size_t)blockIdx.x * blockDim.x + threadIdx.x; ib < n; ib += U * stride) {
     double v[U][3];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const size_t i = ib + u * stride;
+      const double *q = p + 3 * (i < n ? i : n - 1);
 #pragma unroll
-      for (int a = 0; a < 3; ++a) v[u][a] = i < n ? p[3 * i + a] : INFINITY;
+      for (int a = 0; a < 3; ++a) v[u][a] = q[a];
+      if (i >= n) v[u][0] = v[u][1] = v[u][2] = INFINITY;
     }
 #pragma unroll
     for (int u = 0; u < U; ++u)
@@ -438,10 +445,12 @@ __device__ __forceinline__ void bin_chunk(const BinSide &S, int blk, const GridP
   const int bd = (int)blockDim.x;
   for (int ib = i0; ib < i1; ib += kBinUnroll * bd) {
     P3 v[kBinUnroll];
+    // every load issued unconditionally from a clamped index (r5, as in
+    // k_bbox_partial); the lanes past the chunk drop theirs below
 #pragma unroll
     for (int u = 0; u < kBinUnroll; ++u) {
       const int i = ib + u * bd + (int)threadIdx.x;
-      if (i < i1) v[u] = *(const P3 *)(S.p + 3 * (size_t)i);
+      v[u] = *(const P3 *)(S.p + 3 * (size_t)min(i, i1 - 1));
     }
 #pragma unroll
     for (int u = 0; u < kBinUnroll; ++u) {
@@ -514,7 +523,7 @@ __global__ __launch_bounds__(256, kBuildMinW) void k_bin_scatter(BinJob J, const
 #pragma unroll
       for (int u = 0; u < kBinUnroll; ++u) {
         const int i = ib + u * bd + (int)threadIdx.x;
-        c[u] = i < i1 ? S.rawcell[i] : 0;
+        c[u] = S.rawcell[min(i, i1 - 1)];  // (clamped, unconditional; dropped below)
       }
 #pragma unroll
       for (int u = 0; u < kBinUnroll; ++u) {
