@@ -596,10 +596,14 @@ __global__ __launch_bounds__(kBinFineThreads, kBuildMinW) void k_bin_fine(BinJob
   int scell[kFineStageHold];
   const int held_end = min(hi, lo + kBinFineHold * bd);
   if (staged) {
+    // (loads issued unconditionally from clamped slots when the bucket is
+    // not empty, as in bin_chunk; the slots past n are never used)
+    if (n > 0) {
 #pragma unroll
-    for (int u = 0; u < kFineStageHold; ++u) {
-      const int sl = u * bd + tid;
-      if (sl < n) scell[u] = side ? qk[lo + sl].cell : src[lo + sl].cell;
+      for (int u = 0; u < kFineStageHold; ++u) {
+        const int sl = lo + min(u * bd + tid, n - 1);
+        scell[u] = side ? qk[sl].cell : src[sl].cell;
+      }
     }
 #pragma unroll
     for (int u = 0; u < kFineStageHold; ++u)

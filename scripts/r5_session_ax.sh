@@ -13,7 +13,7 @@ for v in clamp4 head; do
 import csv,re
 for r in csv.DictReader(open('$OUT/tr_${v}_$r/run_kernel_stats.csv')):
     m=re.search(r'k_\w+',r['Name'])
-    if m and m.group(0) in ('k_bbox_partial','k_bin_hist'): print('$v', m.group(0), round(float(r['AverageNs'])/1e3,2))"
+    if m and m.group(0) in ('k_bin_fine','k_bin_hist','k_bin_scatter','k_bbox_partial'): print('$v', m.group(0), round(float(r['AverageNs'])/1e3,2))"
 done
 done
 BENCH_ARGS="" bash scripts/env_ab.sh "$1/ab" 3 "NAVGPU_AB_ARM=clamp" "NAVGPU_LIB=nav-slam_amd/lib/variants/libnavgpu_bbhead.so"
