@@ -160,6 +160,16 @@ int navgpu_kd_query_rows_lazy_dev(navgpu_ctx *ctx, double *tree_pts, int32_t *tr
                                   const double *queries, int R, int C, int32_t *nn_pos,
                                   double *nn_dist, int32_t *mask_out,
                                   int32_t *tree_built);
+/* The same, then each row's correspondence sums of the fast mode
+ * (navgpu_rows_corr_dev with keep = NULL: `ori` the queries' global
+ * coordinates, `sums` 6 doubles per row) in the same launch as the tie
+ * pass (r5: one launch and its gap fewer per K5 frame). Not part of the
+ * reference interface. */
+int navgpu_kd_query_rows_lazy_corr_dev(navgpu_ctx *ctx, double *tree_pts, int32_t *tree_col,
+                                       const int32_t *tree_n, const double *feat_src,
+                                       const double *queries, int R, int C, int32_t *nn_pos,
+                                       double *nn_dist, int32_t *mask_out,
+                                       int32_t *tree_built, const double *ori, double *sums);
 
 /* ---- R7: correspondence dedup per row (src/slam.c:247-284) -------------
  * Over the output of navgpu_kd_query_rows: of the queries of row r whose

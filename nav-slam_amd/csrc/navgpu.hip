@@ -2148,15 +2148,25 @@ __global__ __launch_bounds__(NT) void k_rows_query_screen(
 // column order (the array buildKDTree permutes, utils/kdtree.c:65-82), and
 // ALL its queries are answered by the walk (utils/kdtree.c:110-152), since
 // their positions now index the permuted row. Rows without a tie return.
+__device__ void rows_corr_body(int row, unsigned char *corr_lds, const double *tree_pts,
+                               const int32_t *tree_n, const int32_t *nn_pos,
+                               const double *nn_dist, const double *ori, int C, int HS,
+                               int32_t *keep, double *sums, double *ent, int32_t *ent_n);
+
+// The lazy rows' tie pass: a row whose screen met a tie gets the reference
+// tree and all its queries walked. With `ori` (r5, the fast mode) every row's
+// workgroup then runs the row's correspondences and sums (rows_corr_body,
+// the k_rows_corr launch saved).
 __global__ __launch_bounds__(kRowsBlock) void k_rows_retree(
     double *__restrict__ tree_pts, int32_t *__restrict__ tree_col,
     const int32_t *__restrict__ tree_n, const double *__restrict__ feat_src,
     const double *__restrict__ queries, int C, int32_t *__restrict__ nn_pos,
-    double *__restrict__ nn_dist, int32_t *__restrict__ tie, int32_t *__restrict__ built) {
+    double *__restrict__ nn_dist, int32_t *__restrict__ tie, int32_t *__restrict__ built,
+    const double *__restrict__ ori, int HS, double *__restrict__ sums) {
   const int r = blockIdx.x;
   const int tied = tie[r];
   __syncthreads();  // every thread has read the flag before it is cleared
-  if (!tied) return;  // uniform (a built row's ties were walked by the screen)
+  if (tied) {  // uniform (a built row's ties were walked by the screen)
   if (threadIdx.x == 0) tie[r] = 0;  // zero again for the next call (no memset, r5)
   const RowsLds L = rows_lds(C, kRowsBlock, true);
   const size_t rowoff = (size_t)r * C;
@@ -2233,6 +2243,12 @@ __global__ __launch_bounds__(kRowsBlock) void k_rows_retree(
     }
     nn_pos[rowoff + c] = bpos;
     nn_dist[rowoff + c] = bd;
+  }
+  }
+  if (ori) {
+    __syncthreads();  // the walk's results and the LDS are free for the row's pairs
+    rows_corr_body(r, smem, tree_pts, tree_n, nn_pos, nn_dist, ori, C, HS, nullptr, sums,
+                   nullptr, nullptr);
   }
 }
 
@@ -2613,12 +2629,14 @@ __device__ __forceinline__ uint64_t corr_key_bits(double v) {
   return (uint64_t)__double_as_longlong(v == 0.0 ? 0.0 : v);
 }
 
-__global__ __launch_bounds__(kCorrBlock) void k_rows_corr(
-    const double *__restrict__ tree_pts, const int32_t *__restrict__ tree_n,
-    const int32_t *__restrict__ nn_pos, const double *__restrict__ nn_dist,
-    const double *__restrict__ ori, int C, int HS, int32_t *__restrict__ keep,
-    double *__restrict__ sums, double *__restrict__ ent, int32_t *__restrict__ ent_n) {
-  extern __shared__ __attribute__((aligned(8))) unsigned char corr_lds[];
+// one row's correspondences (the k_rows_corr workgroup's work; r5: also the
+// tail of k_rows_retree for the fast lazy path), LDS from `corr_lds`
+__device__ void rows_corr_body(
+    int row, unsigned char *corr_lds, const double *__restrict__ tree_pts,
+    const int32_t *__restrict__ tree_n, const int32_t *__restrict__ nn_pos,
+    const double *__restrict__ nn_dist, const double *__restrict__ ori, int C, int HS,
+    int32_t *__restrict__ keep, double *__restrict__ sums, double *__restrict__ ent,
+    int32_t *__restrict__ ent_n) {
   unsigned long long *bdist = (unsigned long long *)corr_lds;  // [HS]
   int *owner = (int *)(bdist + HS);                            // [HS]
   int *bcol = owner + HS;                                      // [HS]
@@ -2626,7 +2644,6 @@ __global__ __launch_bounds__(kCorrBlock) void k_rows_corr(
   int *canon = fcol + HS;                                      // [C]
   __shared__ double red[kCorrBlock / kWave][6];
   __shared__ int cscan[kCorrBlock / kWave + 1];
-  const int row = blockIdx.x;
   const size_t base = (size_t)row * C;
   const int n = tree_n[row];
   for (int h = threadIdx.x; h < HS; h += blockDim.x) {
@@ -2760,6 +2777,16 @@ __global__ __launch_bounds__(kCorrBlock) void k_rows_corr(
         e[6] = nn_dist[base + kc];
       });
   if (threadIdx.x == 0) ent_n[row] = ne;
+}
+
+__global__ __launch_bounds__(kCorrBlock) void k_rows_corr(
+    const double *__restrict__ tree_pts, const int32_t *__restrict__ tree_n,
+    const int32_t *__restrict__ nn_pos, const double *__restrict__ nn_dist,
+    const double *__restrict__ ori, int C, int HS, int32_t *__restrict__ keep,
+    double *__restrict__ sums, double *__restrict__ ent, int32_t *__restrict__ ent_n) {
+  extern __shared__ __attribute__((aligned(8))) unsigned char corr_lds[];
+  rows_corr_body(blockIdx.x, corr_lds, tree_pts, tree_n, nn_pos, nn_dist, ori, C, HS, keep,
+                 sums, ent, ent_n);
 }
 
 // Concatenates the rows' lists of k_rows_corr (row order) into list[7 * i];
@@ -3354,14 +3381,16 @@ int navgpu_kd_query_rows_dev(navgpu_ctx *ctx, const double *tree_pts,
                            mask_out, nullptr);
 }
 
-int navgpu_kd_query_rows_lazy_dev(navgpu_ctx *ctx, double *tree_pts, int32_t *tree_col,
-                                  const int32_t *tree_n, const double *feat_src,
-                                  const double *queries, int R, int C, int32_t *nn_pos,
-                                  double *nn_dist, int32_t *mask_out, int32_t *tree_built) {
+static int rows_query_lazy(navgpu_ctx *ctx, double *tree_pts, int32_t *tree_col,
+                           const int32_t *tree_n, const double *feat_src,
+                           const double *queries, int R, int C, int32_t *nn_pos,
+                           double *nn_dist, int32_t *mask_out, int32_t *tree_built,
+                           const double *ori, double *sums) {
   ARG_CHECK(ctx);
   RC(check_rows_shape(R, C, true));
   if ((size_t)R * C == 0) return NAVGPU_OK;
   ARG_CHECK(tree_col);
+  ARG_CHECK(!ori || (sums && C <= kMaxRowCols));
   int32_t *tie;
   RC(ws(ctx, kRowTieLazy, (size_t)R, &tie));
   if (tie != ctx->lazy_tie || R > ctx->lazy_tie_rows) {  // a new buffer: zero it once
@@ -3372,18 +3401,39 @@ int navgpu_kd_query_rows_lazy_dev(navgpu_ctx *ctx, double *tree_pts, int32_t *tr
   RC(rows_query_launch(ctx, tree_pts, tree_n, feat_src, queries, R, C, nn_pos, nn_dist,
                        mask_out, tie, tree_col, tree_built));
   const RowsLds L = rows_lds(C, kRowsBlock, true);
-  if (L.total > lds_limit()) {
-    set_err("rows_query_lazy: C=%d needs %d B of LDS (device limit %d)", C, L.total,
-            lds_limit());
+  // (with ori: the rows' correspondences in the same launch, from the same LDS)
+  int HS = 64;
+  while (HS < 2 * C) HS <<= 1;
+  const int lds = ori ? std::max(L.total, HS * (8 + 4 + 4 + 4) + 4 * C) : L.total;
+  if (lds > lds_limit()) {
+    set_err("rows_query_lazy: C=%d needs %d B of LDS (device limit %d)", C, lds, lds_limit());
     return NAVGPU_ERANGE;
   }
-  RC(set_lds(k_rows_retree, L.total));
+  RC(set_lds(k_rows_retree, lds));
   TimedRegion tr(ctx, "rows_retree");
-  hipLaunchKernelGGL(k_rows_retree, dim3(R), dim3(kRowsBlock), L.total, ctx->stream, tree_pts,
+  hipLaunchKernelGGL(k_rows_retree, dim3(R), dim3(kRowsBlock), lds, ctx->stream, tree_pts,
                      tree_col, tree_n, feat_src, queries, C, nn_pos, nn_dist,
-                     tie, tree_built);
+                     tie, tree_built, ori, HS, sums);
   CHECK_LAUNCH("k_rows_retree");
   return NAVGPU_OK;
+}
+
+int navgpu_kd_query_rows_lazy_dev(navgpu_ctx *ctx, double *tree_pts, int32_t *tree_col,
+                                  const int32_t *tree_n, const double *feat_src,
+                                  const double *queries, int R, int C, int32_t *nn_pos,
+                                  double *nn_dist, int32_t *mask_out, int32_t *tree_built) {
+  return rows_query_lazy(ctx, tree_pts, tree_col, tree_n, feat_src, queries, R, C, nn_pos,
+                         nn_dist, mask_out, tree_built, nullptr, nullptr);
+}
+
+int navgpu_kd_query_rows_lazy_corr_dev(navgpu_ctx *ctx, double *tree_pts, int32_t *tree_col,
+                                       const int32_t *tree_n, const double *feat_src,
+                                       const double *queries, int R, int C, int32_t *nn_pos,
+                                       double *nn_dist, int32_t *mask_out, int32_t *tree_built,
+                                       const double *ori, double *sums) {
+  ARG_CHECK(ori && sums);
+  return rows_query_lazy(ctx, tree_pts, tree_col, tree_n, feat_src, queries, R, C, nn_pos,
+                         nn_dist, mask_out, tree_built, ori, sums);
 }
 
 int navgpu_rows_corr_dev(navgpu_ctx *ctx, const double *tree_pts,

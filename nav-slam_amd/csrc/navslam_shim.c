@@ -141,6 +141,14 @@ static int host_trees(void)
     return !(q && *q == '0');
 }
 
+/* Fast mode on lazy rows: the row sums in the tie pass's launch (default), or
+ * NAVSLAM_LAZY_CORR=0 for the separate k_rows_corr launch (r5 A/B knob) */
+static int lazy_corr(void)
+{
+    const char *q = getenv("NAVSLAM_LAZY_CORR");
+    return !(q && *q == '0');
+}
+
 /* ------------------------------------- host KDNode blocks + registry */
 /* Every tree this library hands out is one malloc'd block of KDNode laid
  * out in the implicit order (node of [lo,hi) at lo+(hi-lo)/2), linked like
@@ -511,11 +519,12 @@ void slam_mapping(SLAM_attr *attr, Pos pos, PointCloud *lidarPointCloud)
  * here), so no cancellation and never negative (exact in real arithmetic;
  * rounding differs from the reference's sequential sums). */
 static Pos localization_fast(SLAM_attr *attr, slam_state *s, double transform[6],
-                             Pos pos_last)
+                             Pos pos_last, int corr_done)
 {
     navgpu_ctx *c = ctx();
-    CK(navgpu_rows_corr_dev(c, s->d_tree, s->d_tn, s->d_pos, s->d_dist, s->d_global,
-                            ROWS, COLS, NULL, s->h_sums_pin ? s->h_sums_pin : s->d_sums));
+    if (!corr_done) /* (the lazy rows' query launched it with their tie pass) */
+        CK(navgpu_rows_corr_dev(c, s->d_tree, s->d_tn, s->d_pos, s->d_dist, s->d_global,
+                                ROWS, COLS, NULL, s->h_sums_pin ? s->h_sums_pin : s->d_sums));
     if (!s->h_sums_pin)
         CK(navgpu_download(c, s->h_sums, s->d_sums, sizeof(s->h_sums)));
     CK(navgpu_sync(c));
@@ -620,15 +629,23 @@ Pos slam_localization(SLAM_attr *attr, PointCloud *lidarPointCloud,
         CK(navgpu_upload(c, s->d_tn, (int32_t[ROWS]){0}, 4 * ROWS));
         s->have_trees = 1;
     }
-    if (s->lazy)
+    const int fast = adam_fast();
+    int corr_done = 0;
+    if (s->lazy && fast && lazy_corr()) { /* the fast mode's row sums in the tie pass's launch */
+        CK(navgpu_kd_query_rows_lazy_corr_dev(c, s->d_tree, s->d_tcol, s->d_tn, s->d_lidar,
+                                              s->d_last, ROWS, COLS, s->d_pos, s->d_dist, NULL,
+                                              s->d_built, s->d_global,
+                                              s->h_sums_pin ? s->h_sums_pin : s->d_sums));
+        corr_done = 1;
+    } else if (s->lazy)
         CK(navgpu_kd_query_rows_lazy_dev(c, s->d_tree, s->d_tcol, s->d_tn, s->d_lidar,
                                          s->d_last, ROWS, COLS, s->d_pos, s->d_dist, NULL,
                                          s->d_built));
     else
         CK(navgpu_kd_query_rows_dev(c, s->d_tree, s->d_tn, s->d_lidar, s->d_last,
                                     ROWS, COLS, s->d_pos, s->d_dist, NULL));
-    if (adam_fast())
-        return localization_fast(attr, s, transform, pos_last);
+    if (fast)
+        return localization_fast(attr, s, transform, pos_last, corr_done);
     /* GPU: the reference's correspondence list (src/slam.c:235-284), built
      * and compacted in its first-insertion order on the device; only the
      * list itself comes back */

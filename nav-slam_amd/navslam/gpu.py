@@ -49,6 +49,9 @@ def _declare(L):
                                                  _vp, _vp, _vp, _vp, _vp]),
         "navgpu_kd_query_rows_lazy_dev": (C.c_int, [_vp, _vp, _vp, _vp, _vp, _vp,
                                                     C.c_int, C.c_int, _vp, _vp, _vp, _vp]),
+        "navgpu_kd_query_rows_lazy_corr_dev": (C.c_int, [_vp, _vp, _vp, _vp, _vp, _vp,
+                                                         C.c_int, C.c_int, _vp, _vp, _vp, _vp,
+                                                         _vp, _vp]),
         "navgpu_rows_corr_dev": (C.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, C.c_int,
                                            C.c_int, _vp, _vp]),
         "navgpu_rows_corr_list_dev": (C.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, C.c_int,
@@ -299,6 +302,13 @@ class NavGpu:
             self.h, _ptr(tree_pts), _ptr(tree_col), _ptr(tree_n), _ptr(feat_src),
             _ptr(queries), R, Cc, _ptr(nn_pos), _ptr(nn_dist), _ptr(mask), _ptr(built)),
             "kd_query_rows_lazy_dev")
+
+    def kd_query_rows_lazy_corr_dev(self, tree_pts, tree_col, tree_n, feat_src, queries, R, Cc,
+                                    nn_pos, nn_dist, mask, built, ori, sums):
+        self._check(self.L.navgpu_kd_query_rows_lazy_corr_dev(
+            self.h, _ptr(tree_pts), _ptr(tree_col), _ptr(tree_n), _ptr(feat_src),
+            _ptr(queries), R, Cc, _ptr(nn_pos), _ptr(nn_dist), _ptr(mask), _ptr(built),
+            _ptr(ori), _ptr(sums)), "kd_query_rows_lazy_corr_dev")
 
     def rows_corr_dev(self, tree_pts, tree_n, nn_pos, nn_dist, ori, R, Cc, keep, sums):
         self._check(self.L.navgpu_rows_corr_dev(

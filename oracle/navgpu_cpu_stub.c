@@ -383,3 +383,16 @@ int navgpu_kd_query_rows_lazy_dev(navgpu_ctx *ctx, double *tree_pts, int32_t *tr
     return navgpu_kd_query_rows_dev(ctx, tree_pts, tree_n, feat_src, queries, R, C, nn_pos,
                                     nn_dist, mask_out);
 }
+
+int navgpu_kd_query_rows_lazy_corr_dev(navgpu_ctx *ctx, double *tree_pts, int32_t *tree_col,
+                                       const int32_t *tree_n, const double *feat_src,
+                                       const double *queries, int R, int C, int32_t *nn_pos,
+                                       double *nn_dist, int32_t *mask_out,
+                                       int32_t *tree_built, const double *ori, double *sums)
+{
+    int rc = navgpu_kd_query_rows_lazy_dev(ctx, tree_pts, tree_col, tree_n, feat_src, queries,
+                                           R, C, nn_pos, nn_dist, mask_out, tree_built);
+    if (rc != NAVGPU_OK)
+        return rc;
+    return navgpu_rows_corr_dev(ctx, tree_pts, tree_n, nn_pos, nn_dist, ori, R, C, NULL, sums);
+}

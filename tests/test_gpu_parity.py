@@ -542,6 +542,47 @@ def test_lazy_rows_vs_oracle(gpu, orc, seed, integer_mm, R, Cc):
         assert rebuilt > 0, rebuilt
 
 
+@pytest.mark.parametrize("seed,integer_mm", [(5, True), (9, True), (5, False)])
+def test_lazy_rows_fused_corr_equals_separate(gpu, seed, integer_mm):
+    """kd_query_rows_lazy_corr_dev (the fast mode's row sums in the tie
+    pass's launch, r5) against kd_query_rows_lazy_dev + rows_corr_dev on the
+    same compacted rows: positions, distances, rebuilt rows and the six sums
+    per row bit-identical, with ties (integer-mm, most rows rebuilt) and
+    without."""
+    import torch
+    from navslam.synth import l9_pair
+    R, Cc = 128, 2048
+    lid, lid2 = l9_pair(R, Cc, seed=seed, integer_mm=integer_mm)
+    dev = torch.device("cuda")
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+    d_lid, d_lid2 = t(lid), t(lid2)
+    ori = t(lid2 + np.array([3.0, -1.0, 0.5]))
+    out = {}
+    for fused in (False, True):
+        tree = torch.zeros((R, Cc, 3), dtype=torch.float64, device=dev)
+        tcol = torch.zeros((R, Cc), dtype=torch.int32, device=dev)
+        tn = torch.zeros(R, dtype=torch.int32, device=dev)
+        built = torch.zeros(R, dtype=torch.int32, device=dev)
+        pos = torch.zeros((R, Cc), dtype=torch.int32, device=dev)
+        dist = torch.zeros((R, Cc), dtype=torch.float64, device=dev)
+        sums = torch.zeros((R, 6), dtype=torch.float64, device=dev)
+        torch.cuda.synchronize()
+        gpu.kd_compact_rows_dev(d_lid, d_lid, R, Cc, tree, tcol, tn, None, built)
+        if fused:
+            gpu.kd_query_rows_lazy_corr_dev(tree, tcol, tn, d_lid2, d_lid2, R, Cc, pos, dist,
+                                            None, built, ori, sums)
+        else:
+            gpu.kd_query_rows_lazy_dev(tree, tcol, tn, d_lid2, d_lid2, R, Cc, pos, dist,
+                                       None, built)
+            gpu.rows_corr_dev(tree, tn, pos, dist, ori, R, Cc, None, sums)
+        gpu.sync()
+        out[fused] = [x.cpu().numpy() for x in (tree, tcol, built, pos, dist, sums)]
+    for a, b, nm in zip(out[False], out[True], ("tree", "cols", "built", "pos", "dist", "sums")):
+        _eq(b, a, nm)
+    if integer_mm:
+        assert out[True][2].sum() > 0  # some rows met a tie and were rebuilt
+
+
 # ---------------------------------------------------------- global k-NN
 @pytest.mark.parametrize("k", [1, 3, 8, 16])
 def test_knn_vs_brute(kgpu, orc, k):
