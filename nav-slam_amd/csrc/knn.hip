@@ -589,6 +589,14 @@ __global__ __launch_bounds__(kBinFineThreads, kBuildMinW) void k_bin_fine(BinJob
   const BinPt *src = S.bin;
   const QKey *qk = S.key;
   const int bd = (int)blockDim.x, tid = (int)threadIdx.x;
+  if (n == 0) {
+    // an empty bucket (about half of them: the buckets span the cell cap,
+    // twice the grid's cells): its cells all start at lo, no count or scan
+    if (S.start)
+      for (int j = tid; j < ncell; j += bd)
+        if (base + j < nscan) S.start[base + j] = lo;
+    return;
+  }
   for (int j = tid; j < ncell; j += bd) cnt[j] = 0;
   __syncthreads();
   // unstaged: queries hold only their cell (the placement writes the position)
