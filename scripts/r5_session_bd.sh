@@ -1,5 +1,5 @@
 #!/bin/bash
-# k_bin_fine empty-bucket shortcut: k-NN tests, then K3 A/B against HEAD's build (variants/old)
+# binning passes skip the unused buckets: k-NN tests, then K3 A/B against HEAD's build (variants/old)
 OUT=gpurun_out/$1; mkdir -p "$OUT"
 export PYTHONUNBUFFERED=1 NAVSLAM_QUIET=1
 D=nav-slam_amd/lib/variants/old
