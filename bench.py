@@ -22,8 +22,10 @@ alternate over three library contexts, each with its own stream, workspace
 and outputs, so one pair's memory-bound index build overlaps the previous
 pairs' latency-bound queries. Every step still processes one whole pair.
 
-Launch: python bench.py [--gpus N --steps K --warmup W]; for N > 1 under
-torch.distributed.run (one rank per GPU, RCCL).
+Launch: python bench.py [--gpus N --steps K --warmup W]. For N > 1 either
+under torch.distributed.run (--nproc-per-node N, one rank per GPU, RCCL), or
+plain `python bench.py --gpus N`, which starts that launcher itself as a child
+process; a WORLD_SIZE that differs from --gpus is an error.
 """
 import argparse
 import json
@@ -95,6 +97,9 @@ def parse():
     p.add_argument("--no-stream-copy", action="store_true",
                    help="skip the STREAM-copy ceiling measurement")
     p.add_argument("--json-out", default=None)
+    p.add_argument("--dry-run", action="store_true",
+                   help="rank plumbing only (no GPU): every rank joins a gloo group, takes "
+                        "its K4 shard of --pairs and reports; rank 0 prints one JSON line")
     return p.parse_args()
 
 
@@ -103,6 +108,71 @@ def dist_env():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     return ws, rank, local
+
+
+def _free_port():
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(a):
+    """`--gpus N` (N > 1) run without a launcher: start N rank processes
+    through torch.distributed.run as ONE child process (one rank per GPU,
+    rendezvous on 127.0.0.1) and return its exit code. Nothing here touches
+    the GPU: the parent only waits (no exec from a process that initialised
+    HIP)."""
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={a.gpus}", "--master-addr", "127.0.0.1",
+           "--master-port", str(_free_port()), os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.run(cmd).returncode
+
+
+def check_ranks(a, ws, local):
+    """The rank count must be what --gpus asks for, and every rank needs its
+    own visible device (torch.cuda.device_count() does not initialise HIP on
+    this image). Returns an error message, or None."""
+    if ws != a.gpus:
+        return (f"bench.py: --gpus {a.gpus} but WORLD_SIZE={ws}; launch "
+                f"`python bench.py --gpus N` (it starts the N ranks itself) or "
+                f"torch.distributed.run with --nproc-per-node equal to --gpus")
+    if a.dry_run:
+        return None
+    import torch
+    nd = torch.cuda.device_count()
+    if local >= nd:
+        return (f"bench.py: rank with LOCAL_RANK={local} of --gpus {a.gpus}, but only {nd} "
+                "device(s) visible")
+    return None
+
+
+def run_dry(a, ws, rank):
+    """--dry-run: the K4 rank plumbing on gloo (CPU): every rank takes its
+    contiguous shard of --pairs; the ranks' (rank, lo, hi) are all-gathered
+    and rank 0 returns them."""
+    import torch
+    import torch.distributed as dist
+    from navslam import shard
+    if ws > 1:
+        dist.init_process_group("gloo")
+    lo, hi = shard.shard_pairs(a.pairs, ws, rank)
+    mine = torch.tensor([rank, lo, hi], dtype=torch.int64)
+    if ws > 1:
+        parts = [torch.empty_like(mine) for _ in range(ws)]
+        dist.all_gather(parts, mine)
+    else:
+        parts = [mine]
+    total = shard.sum_over_ranks(hi - lo, torch.device("cpu"))
+    out = None
+    if rank == 0:
+        out = {"dry_run": True, "n_gpus": ws, "gpus_requested": a.gpus,
+               "ranks_reported": [p.tolist() for p in parts], "pairs": int(total),
+               "workload": a.workload}
+    if ws > 1:
+        dist.destroy_process_group()
+    return out
 
 
 def host_info():
@@ -469,7 +539,18 @@ def cpu_baseline_k5(frames, F, nf, gpu_poses):
 
 def main():
     a = parse()
+    if "WORLD_SIZE" not in os.environ and a.gpus > 1:
+        sys.exit(launch_ranks(a))
     ws, rank, local = dist_env()
+    err = check_ranks(a, ws, local)
+    if err is not None:
+        print(err, file=sys.stderr, flush=True)
+        sys.exit(2)
+    if a.dry_run:
+        out = run_dry(a, ws, rank)
+        if out is not None:
+            print(json.dumps(out), flush=True)
+        return out
     if a.workload == "k5":
         import torch
         import torch.distributed as dist

@@ -2153,7 +2153,14 @@ static int knn_run(navgpu_ctx *ctx, const double *tgt, size_t nt, const double *
                    size_t nq, int k, int32_t *idx, double *dist) {
   ARG_CHECK(ctx && k >= 1 && k <= 16);
   ARG_CHECK(nt < (size_t)INT32_MAX / 2 && nq < (size_t)INT32_MAX / 2);
-  if (!nq) return NAVGPU_OK;
+  if (!nq) {
+    // an empty call is clean: its counters (navgpu_knn_check reads the
+    // error flag of the LAST call) are zeroed, not left from the previous one
+    int *counters;
+    RC(ws(ctx, kStats, 16, &counters));
+    HIP_TRY(hipMemsetAsync(counters, 0, 16 * sizeof(int), ctx->stream));
+    return NAVGPU_OK;
+  }
   ARG_CHECK(queries && idx && dist && (tgt || nt == 0));
   const double occ = ctx->knn_occ;
   const int sx = ctx->knn_sx;
@@ -2214,13 +2221,14 @@ static int knn_run(navgpu_ctx *ctx, const double *tgt, size_t nt, const double *
   RC(ws(ctx, kQSort, nq, &qcell));
   int *qraw;
   RC(ws(ctx, kQSlot, nq, &qraw));
-  const int mode = ctx->knn_mode;
   // k_knng's row neighbourhood lists: 9 positions per target, and g0 + 1
-  // column starts per grid row (rows * (g0 + 1) <= 2 ncells <= 2 cap)
+  // column starts per grid row (rows * (g0 + 1) <= 2 ncells <= 2 cap). A
+  // target cloud whose lists would pass the int32 range (> ~238M points)
+  // takes k_knnw (mode 1), which has no lists.
   int *npg = nullptr, *gl = nullptr;
   const long long ngl = std::max<long long>(9LL * (long long)nt, 1);
+  const int mode = (ctx->knn_mode == 2 && ngl >= INT32_MAX) ? 1 : ctx->knn_mode;
   if (mode == 2) {
-    ARG_CHECK(ngl < INT32_MAX);
     RC(ws(ctx, kNpg, 2 * (size_t)cap + 2, &npg));
     RC(ws(ctx, kGl, (size_t)ngl, &gl));
   }

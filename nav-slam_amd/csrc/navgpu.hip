@@ -3398,8 +3398,10 @@ static int rows_query_lazy(navgpu_ctx *ctx, double *tree_pts, int32_t *tree_col,
     ctx->lazy_tie = tie;
     ctx->lazy_tie_rows = R;
   }
-  RC(rows_query_launch(ctx, tree_pts, tree_n, feat_src, queries, R, C, nn_pos, nn_dist,
-                       mask_out, tie, tree_col, tree_built));
+  // Everything that can refuse the call is checked BEFORE the screen runs:
+  // the screen sets tie flags that only k_rows_retree clears, so a refusal
+  // between the two would leave them set for the next call on this context,
+  // which would then rebuild already-built rows from tree order.
   const RowsLds L = rows_lds(C, kRowsBlock, true);
   // (with ori: the rows' correspondences in the same launch, from the same LDS)
   int HS = 64;
@@ -3410,6 +3412,8 @@ static int rows_query_lazy(navgpu_ctx *ctx, double *tree_pts, int32_t *tree_col,
     return NAVGPU_ERANGE;
   }
   RC(set_lds(k_rows_retree, lds));
+  RC(rows_query_launch(ctx, tree_pts, tree_n, feat_src, queries, R, C, nn_pos, nn_dist,
+                       mask_out, tie, tree_col, tree_built));
   TimedRegion tr(ctx, "rows_retree");
   hipLaunchKernelGGL(k_rows_retree, dim3(R), dim3(kRowsBlock), lds, ctx->stream, tree_pts,
                      tree_col, tree_n, feat_src, queries, C, nn_pos, nn_dist,

@@ -228,11 +228,11 @@ struct navgpu_ctx {
   int knn_sx = 3;        // x cells per h (NAVGPU_KNN_SX; r4: 3 -> build -5 us, query same)
   int knn_mode = 2;      // query pass: 2 = k_knng (row lists, r5), 1 = k_knnw (NAVGPU_KNN_MODE)
   bool knn_stats = false;
-  bool pair_side = true;
+  bool pair_side = true;  // pair curvature on the side stream (NAVGPU_PAIR_SIDE=0: on this one)
   // the lazy K5 query's tie flags (kRowTieLazy): zeroed once, then cleared by
   // k_rows_retree as it reads them, so no memset per call
   int32_t *lazy_tie = nullptr;
-  int lazy_tie_rows = 0;  // pair curvature on the side stream (NAVGPU_PAIR_SIDE=0: on this one)
+  int lazy_tie_rows = 0;  // rows the tie buffer was zeroed for
   int screen_rows = 0, screen_S = 0;  // last screened rows_match call (tie diagnostic)
 };
 

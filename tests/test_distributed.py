@@ -86,3 +86,37 @@ def test_k4_shard_and_gather_gloo_world2(orc, pairs):
             for i in range(np.subtract(*shard.shard_pairs(pairs, world, r)[::-1]))}
     for slot in set(range(world * pmax)) - used:   # padding of the ragged tail
         assert (gi[slot] == -1).all()
+
+
+def _bench_cmd(*extra):
+    import sys
+    return [sys.executable, os.path.join(os.path.dirname(os.path.dirname(__file__)), "bench.py"),
+            "--dry-run", "--workload", "k4", "--pairs", "5"] + list(extra)
+
+
+def test_bench_gpus_launches_that_many_ranks():
+    """`bench.py --gpus 2` without a launcher starts 2 ranks itself (a
+    torch.distributed.run child), and both report (gloo, no GPU)."""
+    import json
+    import subprocess
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    r = subprocess.run(_bench_cmd("--gpus", "2"), env=env, capture_output=True, text=True,
+                       timeout=240)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1
+    out = lines[0]
+    assert out["n_gpus"] == 2 and out["gpus_requested"] == 2
+    assert sorted(x[0] for x in out["ranks_reported"]) == [0, 1]
+    assert [x[1:] for x in sorted(out["ranks_reported"])] == [[0, 3], [3, 5]]
+    assert out["pairs"] == 5
+
+
+def test_bench_world_size_mismatch_is_an_error():
+    import subprocess
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run(_bench_cmd("--gpus", "2"), env=env, capture_output=True, text=True,
+                       timeout=120)
+    assert r.returncode == 2
+    assert "WORLD_SIZE=1" in r.stderr

@@ -583,6 +583,60 @@ def test_lazy_rows_fused_corr_equals_separate(gpu, seed, integer_mm):
         assert out[True][2].sum() > 0  # some rows met a tie and were rebuilt
 
 
+def test_lazy_rows_refused_fused_call_leaves_context_clean(gpu, orc):
+    """a fused lazy call the library refuses (C = 2100: its hash
+    table needs more LDS than a workgroup has) must not leave tie flags
+    behind. Rows built by an earlier lazy query (built = 1) are then walked
+    as they stand by the next valid query on the same context, not rebuilt
+    from tree order: trees, positions and distances unchanged, and equal to
+    the oracle's KD walk."""
+    import torch
+    from navslam.gpu import NavGpuError
+    from navslam.synth import l9_pair
+    R, Cc = 8, 2048
+    lid, lid2 = l9_pair(R, Cc, seed=5, integer_mm=True)
+    dev = torch.device("cuda")
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+    d_lid, d_lid2 = t(lid), t(lid2)
+    z = lambda shape, dt: torch.zeros(shape, dtype=dt, device=dev)
+    tree, tcol = z((R, Cc, 3), torch.float64), z((R, Cc), torch.int32)
+    tn, built = z(R, torch.int32), z(R, torch.int32)
+    pos, dist = z((R, Cc), torch.int32), z((R, Cc), torch.float64)
+    torch.cuda.synchronize()
+    gpu.kd_compact_rows_dev(d_lid, d_lid, R, Cc, tree, tcol, tn, None, built)
+    gpu.kd_query_rows_lazy_dev(tree, tcol, tn, d_lid2, d_lid2, R, Cc, pos, dist, None, built)
+    gpu.sync()
+    assert built.sum().item() > 0  # integer-mm: some rows met a tie and hold their tree
+    tree1, tcol1, pos1, dist1 = tree.clone(), tcol.clone(), pos.clone(), dist.clone()
+    # the refused call: tie-heavy rows of 2100 columns, fused correspondences
+    C2 = 2100
+    a2, b2 = l9_pair(R, C2, seed=9, integer_mm=True)
+    e_tree, e_col = z((R, C2, 3), torch.float64), z((R, C2), torch.int32)
+    e_tn, e_built = z(R, torch.int32), z(R, torch.int32)
+    gpu.kd_compact_rows_dev(t(a2), t(a2), R, C2, e_tree, e_col, e_tn, None, e_built)
+    gpu.sync()
+    with pytest.raises(NavGpuError):
+        gpu.kd_query_rows_lazy_corr_dev(e_tree, e_col, e_tn, t(b2), t(b2), R, C2,
+                                        z((R, C2), torch.int32), z((R, C2), torch.float64),
+                                        None, e_built, t(b2), z((R, 6), torch.float64))
+    gpu.sync()
+    gpu.kd_query_rows_lazy_dev(tree, tcol, tn, d_lid2, d_lid2, R, Cc, pos, dist, None, built)
+    gpu.sync()
+    _eq(tree.cpu().numpy(), tree1.cpu().numpy(), "after the refused call: rows unchanged")
+    _eq(tcol.cpu().numpy(), tcol1.cpu().numpy(), "after the refused call: columns unchanged")
+    _eq(pos.cpu().numpy(), pos1.cpu().numpy(), "after the refused call: positions")
+    _eq(dist.cpu().numpy(), dist1.cpu().numpy(), "after the refused call: distances")
+    fm, qm = orc.extract_feature(lid), orc.extract_feature(lid2)
+    tr, tnn, ps, ds = (x.cpu().numpy() for x in (tree, tn, pos, dist))
+    for r in range(R):
+        rt, _ = orc.kd_build(lid[r, np.nonzero(fm[r] == 1)[0]])
+        for c in np.nonzero(qm[r] == 1)[0]:
+            p, d = orc.kd_nn(rt, lid2[r, c])
+            assert ds[r, c] == d, (r, c)
+            if p >= 0:
+                assert tr[r, ps[r, c]].tobytes() == rt[p].tobytes(), (r, c)
+
+
 # ---------------------------------------------------------- global k-NN
 @pytest.mark.parametrize("k", [1, 3, 8, 16])
 def test_knn_vs_brute(kgpu, orc, k):
@@ -1045,16 +1099,22 @@ def test_shim_copy_paths_vs_oracle(monkeypatch, d2h, trees):
         last_g, last_o = meas, om
 
 
-@pytest.mark.parametrize("trees", ["1", "0"])
-def test_shim_localise_twice_between_mappings(monkeypatch, trees):
+@pytest.mark.parametrize("trees,adam", [("1", "exact"), ("0", "exact"), ("0", "fast")])
+def test_shim_localise_twice_between_mappings(monkeypatch, trees, adam):
     """Two localisations against the same map (no slam_mapping between them,
     a caller the reference allows): with lazy rows (NAVSLAM_HOST_TREES=0) the
     first call turns tied rows into the reference tree in place, and the
     second must walk that tree, not rebuild one from the permuted order
     (ADVICE r4). Integer-mm frames make ties common. Every pose and error
-    against the oracle's slam.c, for host trees on and off."""
+    against the oracle's slam.c, for host trees on and off; in fast mode
+    (the fused lazy query + row sums) the correspondence counts
+    exactly and the poses within the fast mode's 1e-6."""
     monkeypatch.setenv("NAVSLAM_QUIET", "1")
     monkeypatch.setenv("NAVSLAM_HOST_TREES", trees)
+    if adam == "fast":
+        monkeypatch.setenv("NAVSLAM_ADAM", "fast")
+    else:
+        monkeypatch.delenv("NAVSLAM_ADAM", raising=False)
     from pyoracle import Oracle, OracleSlam
     from shimlib import Pos, Shim
     from navslam.synth import l9_stream
@@ -1072,9 +1132,18 @@ def test_shim_localise_twice_between_mappings(monkeypatch, trees):
     for f in range(1, F):
         for rep in range(2):  # the same map twice; the second starts at the first's answer
             meas = sh.L.slam_localization(C.byref(attr), C.byref(pcs[f]), last_g, last_g)
-            om, _, _ = s.localization(frames[f], last_o, last_o)
-            _eq(np.array(meas.tolist()), om, f"frame {f} localisation {rep} pose")
-            assert attr.error == s.error, f"frame {f} localisation {rep} error"
+            om, _, ncp = s.localization(frames[f], last_o, last_o)
+            if adam == "fast":
+                np.testing.assert_allclose(np.array(meas.tolist()), om, rtol=0, atol=1e-6,
+                                           err_msg=f"frame {f} localisation {rep} pose")
+                assert sh.last_frame_stats()[1] == ncp, f"frame {f} localisation {rep}"
+                assert abs(attr.error - s.error) <= 1e-9 * max(1.0, s.error)
+                # (the chain continues from the oracle's pose, so both sides
+                # localise the same frame from the same start)
+                meas = Pos.of(om)
+            else:
+                _eq(np.array(meas.tolist()), om, f"frame {f} localisation {rep} pose")
+                assert attr.error == s.error, f"frame {f} localisation {rep} error"
             last_g, last_o = meas, om
         sh.L.slam_mapping(C.byref(attr), meas, C.byref(pcs[f]))
         s.mapping(om, frames[f])
@@ -1252,16 +1321,19 @@ def test_rows_corr_list_matches_reference_list(gpu, orc, integer_mm):
     _eq(got[:, 6], d, "distance")
 
 
-@pytest.mark.parametrize("trees", ["1", "0"])
+@pytest.mark.parametrize("trees,lazy_corr", [("1", "1"), ("0", "1"), ("0", "0")])
 @pytest.mark.parametrize("R,Cc,F,steps", [(54, 42, 4, 9), (128, 2048, 3, 4)])
-def test_shim_l9_stream_fast_adam(monkeypatch, R, Cc, F, steps, trees):
+def test_shim_l9_stream_fast_adam(monkeypatch, R, Cc, F, steps, trees, lazy_corr):
     """NAVSLAM_ADAM=fast (GPU dedup + closed-form Adam sums) on the K5 loop:
     the same correspondence counts as the oracle's slam.c restatement every
     frame, poses within 1e-6 mm / deg (tolerance of the order-free sums,
-    which round differently from the reference's sequential ones)."""
+    which round differently from the reference's sequential ones). Lazy rows
+    with the row sums fused into the tie pass (NAVSLAM_LAZY_CORR=1, default)
+    and as a separate k_rows_corr launch into the pinned sums (=0)."""
     monkeypatch.setenv("NAVSLAM_QUIET", "1")
     monkeypatch.setenv("NAVSLAM_ADAM", "fast")
     monkeypatch.setenv("NAVSLAM_HOST_TREES", trees)
+    monkeypatch.setenv("NAVSLAM_LAZY_CORR", lazy_corr)
     from pyoracle import Oracle, OracleSlam
     from shimlib import Pos, Shim
     from navslam.synth import l9_stream, l9_stream_index
