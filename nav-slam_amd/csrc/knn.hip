@@ -80,10 +80,15 @@ constexpr int kBBoxBlocks = 256;  // bbox partials (every k_bin_hist block reduc
 #ifndef NAVGPU_BBOX_U
 #define NAVGPU_BBOX_U 4
 #endif
+#ifndef NAVGPU_BBOX_THREADS
+#define NAVGPU_BBOX_THREADS 256
+#endif
+constexpr int kBBoxThreads = NAVGPU_BBOX_THREADS;  // threads per k_bbox_partial block
+static_assert(kBBoxThreads % kWave == 0 && kBBoxThreads <= 1024, "bbox block");
 // per-block min/max of the finite coordinates -> part[block][6]
-__global__ __launch_bounds__(256) void k_bbox_partial(const double *__restrict__ p,
-                                                      size_t n, double *__restrict__ part) {
-  __shared__ double s[4][6];
+__global__ __launch_bounds__(kBBoxThreads) void k_bbox_partial(const double *__restrict__ p,
+                                                               size_t n, double *__restrict__ part) {
+  __shared__ double s[kBBoxThreads / kWave][6];
   double v6[6] = {INFINITY, INFINITY, INFINITY, -INFINITY, -INFINITY, -INFINITY};
   // batches of U points per thread, all loads of a batch in flight together,
   // issued unconditionally from clamped indices (r5: a conditional load per
@@ -122,7 +127,7 @@ __global__ __launch_bounds__(256) void k_bbox_partial(const double *__restrict__
   if (threadIdx.x < 6) {
     const int a = threadIdx.x;
     double r = s[0][a];
-    for (int w = 1; w < 4; ++w) r = a < 3 ? fmin(r, s[w][a]) : fmax(r, s[w][a]);
+    for (int w = 1; w < kBBoxThreads / kWave; ++w) r = a < 3 ? fmin(r, s[w][a]) : fmax(r, s[w][a]);
     part[blockIdx.x * 6 + a] = r;
   }
 }
@@ -144,7 +149,7 @@ __device__ void grid_params_block(const GridArgs A, GridParams *out) {
   const int nparts = A.nparts, cap = A.cap, sx = A.sx;
   const double occ = A.occ;
   const size_t n = A.n;
-  __shared__ double s[4][6];
+  __shared__ double s[16][6];  // one row per wave (<= 1024 threads)
   double v6[6] = {INFINITY, INFINITY, INFINITY, -INFINITY, -INFINITY, -INFINITY};
   for (int b = threadIdx.x; b < nparts; b += blockDim.x)
     for (int a = 0; a < 6; ++a)
@@ -410,6 +415,10 @@ __device__ __forceinline__ SRec make_srec(const GridParams &G, bool sglobal, dou
   r.cx = cx;
   return r;
 }
+// k_knng's staged record: the f32 offsets from the grid centre
+__device__ __forceinline__ F3 make_f3(const GridParams &G, double x, double y, double z) {
+  return F3{(float)(x - G.c[0]), (float)(y - G.c[1]), (float)(z - G.c[2])};
+}
 constexpr int kBinMaxShift = 15;
 constexpr int kBinUnroll = kLean ? 4 : 8;  // points per thread with loads in flight
 // (compile-time knobs for A/B variant builds, scripts/build_variants.sh)
@@ -463,7 +472,11 @@ __device__ __forceinline__ void bin_chunk(const BinSide &S, int blk, const GridP
 // Also derives the grid (grid_params_block; block 0 publishes it to *gp and
 // resets the call's k-NN counters) and keeps each query's cell for
 // k_bin_scatter (4 B instead of re-reading its 24-B point).
-__global__ __launch_bounds__(256, kBuildMinW) void k_bin_hist(BinJob J, const GridArgs A,
+#ifndef NAVGPU_BIN_THREADS
+#define NAVGPU_BIN_THREADS 512  // (r6 A/B: k_bin_scatter 25.9 -> 23.9 us against 256; 1024: k_bin_hist 14.8 -> 22)
+#endif
+constexpr int kBinThreads = NAVGPU_BIN_THREADS;  // threads per k_bin_hist / k_bin_scatter block
+__global__ __launch_bounds__(kBinThreads, kBuildMinW) void k_bin_hist(BinJob J, const GridArgs A,
                                                   GridParams *__restrict__ gp,
                                                   int *__restrict__ counters,
                                                   int *__restrict__ table) {
@@ -485,7 +498,7 @@ __global__ __launch_bounds__(256, kBuildMinW) void k_bin_hist(BinJob J, const Gr
   for (int b = threadIdx.x; b < J.nb; b += blockDim.x) table[S.tab + blk * J.nb + b] = hist[b];
 }
 
-__global__ __launch_bounds__(256, kBuildMinW) void k_bin_scatter(BinJob J, const GridParams *__restrict__ gp,
+__global__ __launch_bounds__(kBinThreads, kBuildMinW) void k_bin_scatter(BinJob J, const GridParams *__restrict__ gp,
                                                      const int *__restrict__ offs,
                                                      const int *__restrict__ btot,
                                                      int *__restrict__ bbase) {
@@ -680,7 +693,7 @@ __global__ __launch_bounds__(kBinFineThreads, kBuildMinW) void k_bin_fine(BinJob
         t.cx = e.cell - row * g0;
         S.sorted[lo + j] = t;
         if (S.frec)
-          S.frec[lo + j] = F3{(float)(e.x - G.c[0]), (float)(e.y - G.c[1]), (float)(e.z - G.c[2])};
+          S.frec[lo + j] = make_f3(G, e.x, e.y, e.z);
         else
           S.srec[lo + j] = make_srec(G, J.sglobal, e.x, e.y, e.z, e.cell, lo + j);
       }
@@ -702,7 +715,7 @@ __global__ __launch_bounds__(kBinFineThreads, kBuildMinW) void k_bin_fine(BinJob
       t.cx = e.cell - row * g0;
       S.sorted[pos] = t;
       if (S.frec)
-        S.frec[pos] = F3{(float)(e.x - G.c[0]), (float)(e.y - G.c[1]), (float)(e.z - G.c[2])};
+        S.frec[pos] = make_f3(G, e.x, e.y, e.z);
       else
         S.srec[pos] = make_srec(G, J.sglobal, e.x, e.y, e.z, e.cell, pos);
     }
@@ -1492,6 +1505,158 @@ constexpr bool kNtQ = NAVGPU_KNNG_NT_Q, kNtOut = NAVGPU_KNNG_NT_OUT;
 typedef double d2v __attribute__((ext_vector_type(2)));
 typedef int i4v __attribute__((ext_vector_type(4)));
 
+// The tail of one lane's query in k_knng: the exact f64 stage on
+// the K best keys (their cell-sorted positions from posf(slot)), the
+// certificate that no candidate left out (outside the block, or past the
+// (K+1)-th key) can rank among the K, and the result: into the LDS rows of a
+// chunk done in one round (tstore), else straight to the outputs; an
+// uncertified query goes to k_knn_slow with its K-th dsq bound.
+template <int K, class PosF>
+__device__ __forceinline__ void knng_finish(
+    const uint32_t *key, int ta, int t0, int t1, bool overflow, double Dq, double dl, double Lr,
+    uint32_t vmask, const GridParams &G, const double *qv, int qidx, int qi,
+    const PRec *__restrict__ tsort, int ntg, bool tstore, double *rd, int *ri, int *rq, int lane,
+    int32_t *__restrict__ oidx, double *__restrict__ odist, const KnnLists &L_, int &bad,
+    PosF posf) {
+  bool ok = !overflow && Dq < 1e17;
+  double ed[K];
+  int ei[K];
+  // exact f64 stage on the K best keys
+  if (key[0] != kNoKey) {
+    int gq[K];
+#pragma unroll
+    for (int s = 0; s < K; ++s) {
+      const uint32_t kk = key[s] != kNoKey ? key[s] : key[0];
+      const int p = min(max(ta + (int)(kk & kKeyMask), t0), max(t1 - 1, t0));
+      gq[s] = posf(p);
+    }
+    // all 2 K gathers in flight before any is used
+    double2 gxy[K], gzi[K];
+#pragma unroll
+    for (int s = 0; s < K; ++s) {
+      bad |= (unsigned)gq[s] >= (unsigned)ntg;
+      const PRec *tp = tsort + min(max((kAbl & 1) ? (gq[s] & 1023) : gq[s], 0), max(ntg - 1, 0));
+      gxy[s] = *(const double2 *)&tp->x;
+      gzi[s] = *(const double2 *)&tp->z;
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int s = 0; s < K; ++s) {
+      const bool val = key[s] != kNoKey;
+      const double2 xy = gxy[s], zi = gzi[s];
+      const double pz = zi.x;
+      const int pid = __double2loint(zi.y);
+      const double ddx = xy.x - qv[0], ddy = xy.y - qv[1], ddz = pz - qv[2];
+      const double dsq = ddx * ddx + ddy * ddy + ddz * ddz;  // utils/kdtree.c:16
+      ei[s] = val ? pid : -1;
+      ed[s] = val ? __builtin_sqrt(dsq) : INFINITY;
+      if (val && !(ed[s] < INFINITY)) {  // an inf/NaN distance is never a neighbour (kdtree.c:117)
+        ed[s] = INFINITY;
+        ei[s] = -1;
+        ok = false;
+      }
+    }
+  } else {
+#pragma unroll
+    for (int s = 0; s < K; ++s) {
+      ed[s] = INFINITY;
+      ei[s] = -1;
+    }
+  }
+  // certificate bound on every candidate left out
+  double B = INFINITY;
+  if (Lr < INFINITY) {
+    const double Lg = Lr - 2.0 * G.delta;
+    B = Lg > 0.0 ? Lg * Lg : 0.0;
+  }
+  if (key[K] != kNoKey) {
+    const double V = (double)__uint_as_float(key[K] & vmask);
+    B = fmin(B, V - f32_err(V, dl));
+  }
+  bool sorted = true;
+#pragma unroll
+  for (int s = 1; s < K; ++s) sorted &= !knn_less_bf(ed[s], ei[s], ed[s - 1], ei[s - 1]);
+  for (int pass = 0; pass < K - 1 && __any(!sorted); ++pass) {
+#pragma unroll
+    for (int u = 1; u < K; ++u) knn_cx(ed[u - 1], ei[u - 1], ed[u], ei[u]);
+    sorted = true;
+#pragma unroll
+    for (int s = 1; s < K; ++s) sorted &= !knn_less_bf(ed[s], ei[s], ed[s - 1], ei[s - 1]);
+  }
+  const double dk = ed[K - 1];
+  const double dk2 = dk * dk;
+  if (dk < INFINITY)
+    ok = ok && B > dk2 * (1.0 + 0x1p-46);
+  else
+    ok = ok && B == INFINITY;
+  if (tstore) rq[lane] = ok ? qidx : -1;
+  if (ok && tstore) {
+#pragma unroll
+    for (int s = 0; s < K; s += 2)
+      *(double2 *)(rd + lane * 8 + s) = make_double2(ed[s], ed[s + 1]);
+#pragma unroll
+    for (int s = 0; s < K; s += 4)
+      *(int4 *)(ri + lane * 8 + s) = make_int4(ei[s], ei[s + 1], ei[s + 2], ei[s + 3]);
+  } else if (ok && (!(kAbl & 4) || ed[0] == -1.0)) {
+    const size_t q = (size_t)qidx;
+    if (K % 4 == 0 && L_.vec_out) {
+#pragma unroll
+      for (int s = 0; s < K; s += 4)
+        *(int4 *)(oidx + q * K + s) = make_int4(ei[s], ei[s + 1], ei[s + 2], ei[s + 3]);
+#pragma unroll
+      for (int s = 0; s < K; s += 2)
+        *(double2 *)(odist + q * K + s) = make_double2(ed[s], ed[s + 1]);
+    } else {
+#pragma unroll
+      for (int s = 0; s < K; ++s) {
+        oidx[q * K + s] = ei[s];
+        odist[q * K + s] = ed[s];
+      }
+    }
+  } else if (!ok) {
+    push_slow(L_, qi, (dk < INFINITY && !overflow) ? dk2 * (1.0 + 0x1p-46) : INFINITY);
+  }
+}
+
+// A chunk done in one round writes its results as whole rows (k = 8): lane l
+// left its 8 distances at rd + 8 l, its indices at ri + 8 l and its query in
+// rq[l] (-1: no row; lanes outside the round are marked here, after every
+// lane's reads of the image, which the rows overlap). Instruction i then
+// writes 16-B piece l & 3 of query 16 i + l / 4's distance row and piece
+// l & 1 of query 32 i + l / 2's index row.
+__device__ __forceinline__ void knng_store_rows(const double *rd, const int *ri, int *rq,
+                                                bool active, int lane, int32_t *__restrict__ oidx,
+                                                double *__restrict__ odist) {
+  if (!active) rq[lane] = -1;
+  wave_sync_mem();
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int qa = 16 * i + (lane >> 2), pc = lane & 3;
+    const int q = rq[qa];
+    const double2 v = *(const double2 *)(rd + qa * 8 + 2 * pc);
+    if (q >= 0) {
+      double2 *o = (double2 *)(odist + (size_t)q * 8 + 2 * pc);
+      if (kNtOut)
+        __builtin_nontemporal_store(d2v{v.x, v.y}, (d2v *)o);
+      else
+        *o = v;
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int qa = 32 * i + (lane >> 1), pc = lane & 1;
+    const int q = rq[qa];
+    const int4 v = *(const int4 *)(ri + qa * 8 + 4 * pc);
+    if (q >= 0) {
+      int4 *o = (int4 *)(oidx + (size_t)q * 8 + 4 * pc);
+      if (kNtOut)
+        __builtin_nontemporal_store(i4v{v.x, v.y, v.z, v.w}, (i4v *)o);
+      else
+        *o = v;
+    }
+  }
+}
+
 template <int K>
 __global__ __launch_bounds__(kWave, NAVGPU_KNNG_MINW) void k_knng(
     const GridParams *__restrict__ gp, const int *__restrict__ npg, const int *__restrict__ gl,
@@ -1722,141 +1887,14 @@ __global__ __launch_bounds__(kWave, NAVGPU_KNNG_MINW) void k_knng(
       }
       NV_GT(ts2);
       NV_GADD(5, ts1, ts2);
-      bool ok = !overflow && Dq < 1e17;
-      double ed[K];
-      int ei[K];
-      // exact f64 stage on the K best keys
-      if (key[0] != kNoKey) {
-        int gq[K];
-#pragma unroll
-        for (int s = 0; s < K; ++s) {
-          const uint32_t kk = key[s] != kNoKey ? key[s] : key[0];
-          const int p = min(max(ta + (int)(kk & kKeyMask), t0), max(t1 - 1, t0));
-          gq[s] = __float_as_int(spair[kGZg + (p >> 1) * 4 + 2 + (p & 1)]);
-        }
-        // all 2 K gathers in flight before any is used
-        double2 gxy[K], gzi[K];
-#pragma unroll
-        for (int s = 0; s < K; ++s) {
-          bad |= (unsigned)gq[s] >= (unsigned)ntg;
-          const PRec *tp = tsort + min(max((kAbl & 1) ? (gq[s] & 1023) : gq[s], 0), max(ntg - 1, 0));
-          gxy[s] = *(const double2 *)&tp->x;
-          gzi[s] = *(const double2 *)&tp->z;
-        }
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int s = 0; s < K; ++s) {
-          const bool val = key[s] != kNoKey;
-          const double2 xy = gxy[s], zi = gzi[s];
-          const double pz = zi.x;
-          const int pid = __double2loint(zi.y);
-          const double ddx = xy.x - qv[0], ddy = xy.y - qv[1], ddz = pz - qv[2];
-          const double dsq = ddx * ddx + ddy * ddy + ddz * ddz;  // utils/kdtree.c:16
-          ei[s] = val ? pid : -1;
-          ed[s] = val ? __builtin_sqrt(dsq) : INFINITY;
-          if (val && !(ed[s] < INFINITY)) {  // an inf/NaN distance is never a neighbour (kdtree.c:117)
-            ed[s] = INFINITY;
-            ei[s] = -1;
-            ok = false;
-          }
-        }
-      } else {
-#pragma unroll
-        for (int s = 0; s < K; ++s) {
-          ed[s] = INFINITY;
-          ei[s] = -1;
-        }
-      }
-      // certificate bound on every candidate left out
-      double B = INFINITY;
-      if (Lr < INFINITY) {
-        const double Lg = Lr - 2.0 * G.delta;
-        B = Lg > 0.0 ? Lg * Lg : 0.0;
-      }
-      if (key[K] != kNoKey) {
-        const double V = (double)__uint_as_float(key[K] & vmask);
-        B = fmin(B, V - f32_err(V, dl));
-      }
-      bool sorted = true;
-#pragma unroll
-      for (int s = 1; s < K; ++s) sorted &= !knn_less_bf(ed[s], ei[s], ed[s - 1], ei[s - 1]);
-      for (int pass = 0; pass < K - 1 && __any(!sorted); ++pass) {
-#pragma unroll
-        for (int u = 1; u < K; ++u) knn_cx(ed[u - 1], ei[u - 1], ed[u], ei[u]);
-        sorted = true;
-#pragma unroll
-        for (int s = 1; s < K; ++s) sorted &= !knn_less_bf(ed[s], ei[s], ed[s - 1], ei[s - 1]);
-      }
-      const double dk = ed[K - 1];
-      const double dk2 = dk * dk;
-      if (dk < INFINITY)
-        ok = ok && B > dk2 * (1.0 + 0x1p-46);
-      else
-        ok = ok && B == INFINITY;
-      if (tstore) rq[lane] = ok ? qidx : -1;
-      if (ok && tstore) {
-#pragma unroll
-        for (int s = 0; s < K; s += 2)
-          *(double2 *)(rd + lane * 8 + s) = make_double2(ed[s], ed[s + 1]);
-#pragma unroll
-        for (int s = 0; s < K; s += 4)
-          *(int4 *)(ri + lane * 8 + s) = make_int4(ei[s], ei[s + 1], ei[s + 2], ei[s + 3]);
-      } else if (ok && (!(kAbl & 4) || ed[0] == -1.0)) {
-        const size_t q = (size_t)qidx;
-        if (K % 4 == 0 && L_.vec_out) {
-#pragma unroll
-          for (int s = 0; s < K; s += 4)
-            *(int4 *)(oidx + q * K + s) = make_int4(ei[s], ei[s + 1], ei[s + 2], ei[s + 3]);
-#pragma unroll
-          for (int s = 0; s < K; s += 2)
-            *(double2 *)(odist + q * K + s) = make_double2(ed[s], ed[s + 1]);
-        } else {
-#pragma unroll
-          for (int s = 0; s < K; ++s) {
-            oidx[q * K + s] = ei[s];
-            odist[q * K + s] = ed[s];
-          }
-        }
-      } else if (!ok) {
-        push_slow(L_, qi, (dk < INFINITY && !overflow) ? dk2 * (1.0 + 0x1p-46) : INFINITY);
-      }
+      knng_finish<K>(key, ta, t0, t1, overflow, Dq, dl, Lr, vmask, G, qv, qidx, qi, tsort, ntg,
+                     tstore, rd, ri, rq, lane, oidx, odist, L_, bad, [&](int p) {
+                       return __float_as_int(spair[kGZg + (p >> 1) * 4 + 2 + (p & 1)]);
+                     });
       NV_GT(ts3);
       NV_GADD(6, ts2, ts3);
     }
-    if (tstore) {
-      // (lanes outside the round: no row; written after every lane's reads
-      // of the image, which rq overlaps) then instruction i writes 16-B piece
-      // l & 3 of query 16 i + l / 4's distance row and piece l & 1 of query
-      // 32 i + l / 2's index row
-      if (!(in && lane < lb)) rq[lane] = -1;
-      wave_sync_mem();
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int qa = 16 * i + (lane >> 2), pc = lane & 3;
-        const int q = rq[qa];
-        const double2 v = *(const double2 *)(rd + qa * 8 + 2 * pc);
-        if (q >= 0) {
-          double2 *o = (double2 *)(odist + (size_t)q * 8 + 2 * pc);
-          if (kNtOut)
-            __builtin_nontemporal_store(d2v{v.x, v.y}, (d2v *)o);
-          else
-            *o = v;
-        }
-      }
-#pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        const int qa = 32 * i + (lane >> 1), pc = lane & 1;
-        const int q = rq[qa];
-        const int4 v = *(const int4 *)(ri + qa * 8 + 4 * pc);
-        if (q >= 0) {
-          int4 *o = (int4 *)(oidx + (size_t)q * 8 + 4 * pc);
-          if (kNtOut)
-            __builtin_nontemporal_store(i4v{v.x, v.y, v.z, v.w}, (i4v *)o);
-          else
-            *o = v;
-        }
-      }
-    }
+    if (tstore) knng_store_rows(rd, ri, rq, in && lane < lb, lane, oidx, odist);
     la = lb;
     wave_sync_mem();  // LDS is restaged by the next round
   }
@@ -2228,11 +2266,12 @@ static int knn_run(navgpu_ctx *ctx, const double *tgt, size_t nt, const double *
   int *npg = nullptr, *gl = nullptr;
   const long long ngl = std::max<long long>(9LL * (long long)nt, 1);
   const int mode = (ctx->knn_mode == 2 && ngl >= INT32_MAX) ? 1 : ctx->knn_mode;
-  if (mode == 2) {
+  const bool lists = mode == 2;  // k_knng stages from the row lists
+  if (lists) {
     RC(ws(ctx, kNpg, 2 * (size_t)cap + 2, &npg));
     RC(ws(ctx, kGl, (size_t)ngl, &gl));
   }
-  J.sglobal = mode == 2;
+  J.sglobal = lists;
   J.s[0].p = tgt;
   J.s[1].p = queries;
   J.s[0].start = tstart;
@@ -2259,7 +2298,7 @@ static int knn_run(navgpu_ctx *ctx, const double *tgt, size_t nt, const double *
   {
     TimedRegion tb(ctx, "knn_build");
     if (nt) {
-      hipLaunchKernelGGL(k_bbox_partial, dim3(nparts), dim3(256), 0, s, tgt, nt, part);
+      hipLaunchKernelGGL(k_bbox_partial, dim3(nparts), dim3(kBBoxThreads), 0, s, tgt, nt, part);
       CHECK_LAUNCH("k_bbox_partial");
     }
     GridArgs A;
@@ -2271,13 +2310,13 @@ static int knn_run(navgpu_ctx *ctx, const double *tgt, size_t nt, const double *
     A.n = nt;
     A.nq = nq;
     const dim3 gb(J.s[0].nblk + J.s[1].nblk);
-    hipLaunchKernelGGL(k_bin_hist, gb, dim3(256), 4 * (size_t)J.nb, s, J, A, gp, counters, tab);
+    hipLaunchKernelGGL(k_bin_hist, gb, dim3(kBinThreads), 4 * (size_t)J.nb, s, J, A, gp, counters, tab);
     CHECK_LAUNCH("k_bin_hist");
     const dim3 gc(2 * ((J.nb + kColB - 1) / kColB));
     hipLaunchKernelGGL(k_bin_colscan, gc, dim3(kColB * kColY), 0, s, tab, J.nb, J.s[0].tab,
                        J.s[0].nblk, J.s[1].tab, J.s[1].nblk, btot);
     CHECK_LAUNCH("k_bin_colscan");
-    hipLaunchKernelGGL(k_bin_scatter, gb, dim3(256), 4 * (size_t)J.nb, s, J, gp, (const int *)tab,
+    hipLaunchKernelGGL(k_bin_scatter, gb, dim3(kBinThreads), 4 * (size_t)J.nb, s, J, gp, (const int *)tab,
                        (const int *)btot, bbase);
     CHECK_LAUNCH("k_bin_scatter");
     // staged query placement when its LDS fits beside a 2^shift count table
@@ -2289,7 +2328,7 @@ static int knn_run(navgpu_ctx *ctx, const double *tgt, size_t nt, const double *
     hipLaunchKernelGGL(k_bin_fine, dim3(2 * J.nb), dim3(kBinFineThreads), lds, s, J, gp,
                        (const int *)bbase, nscan, st_q ? kFineStage : 0);
     CHECK_LAUNCH("k_bin_fine");
-    if (mode == 2) {
+    if (lists) {
       // tasks (64 columns of a row) <= 2 cap / 64 + rows; a few per wave
       // (4096 workgroups, one task per wave: build -2 us, bench flat in r5)
       const unsigned nbl = std::min<unsigned>(1024, std::max<unsigned>(1, grid1d(2 * (size_t)cap, 64 * kNbWaves * 2)));
@@ -2298,13 +2337,13 @@ static int knn_run(navgpu_ctx *ctx, const double *tgt, size_t nt, const double *
       CHECK_LAUNCH("k_nb_fill");
     }
   }
-  KnnLists lists;
-  RC(ws(ctx, kSlowQ, nq, &lists.slow_q));
-  RC(ws(ctx, kSlowThr, nq, &lists.slow_thr));
-  lists.n_unstaged = counters;
-  lists.n_slow = counters + 1;
-  lists.err = counters + 2;
-  lists.vec_out = ((uintptr_t)idx % 16 == 0 && (uintptr_t)dist % 16 == 0) ? 1 : 0;
+  KnnLists klists;
+  RC(ws(ctx, kSlowQ, nq, &klists.slow_q));
+  RC(ws(ctx, kSlowThr, nq, &klists.slow_thr));
+  klists.n_unstaged = counters;
+  klists.n_slow = counters + 1;
+  klists.err = counters + 2;
+  klists.vec_out = ((uintptr_t)idx % 16 == 0 && (uintptr_t)dist % 16 == 0) ? 1 : 0;
   TimedRegion tr(ctx, "knn_query");
   const dim3 gs(std::max<unsigned>(1, std::min<unsigned>(2048, grid1d(nq, 256))));
   // one 64-lane block per chunk of 64 cell-sorted queries, chunks dealt to
@@ -2320,12 +2359,12 @@ static int knn_run(navgpu_ctx *ctx, const double *tgt, size_t nt, const double *
       hipLaunchKernelGGL((k_knng<KK>), gg, dim3(kWave), 0, s, gp, (const int *)npg,         \
                          (const int *)gl, (int)ngl, tsort, (const F3 *)srec,                \
                          pack ? 3 : 4, QS, (int)nq, (int)nt, idx,                           \
-                         dist, lists);                                                      \
+                         dist, klists);                                                     \
     else                                                                                    \
       hipLaunchKernelGGL((k_knnw<KK>), gw, bw, 0, s, gp, tstart, tsort, srec, QS, (int)nq,      \
-                         (int)nt, idx, dist, lists);                                        \
+                         (int)nt, idx, dist, klists);                                       \
     hipLaunchKernelGGL((k_knn_slow<KK>), gs, dim3(256), 0, s, gp, tstart, tsort, QS,       \
-                       idx, dist, lists);                                                   \
+                       idx, dist, klists);                                                  \
     break;
   switch (k) {
     KNN_CASE(1)
