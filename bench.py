@@ -419,6 +419,7 @@ def run_k5(a, ws, rank, dev):
     cpu = None
     if not a.no_cpu_baseline and a.cpu_frames > 0:
         cpu = cpu_baseline_k5(frames, F, min(a.cpu_frames, len(poses)), poses)
+    vs_trace = k5_vs_trace(poses, frames, R, Cc, F, 11 + rank, a.warmup)
     # (a region never entered this run, e.g. rows_retree with host trees on,
     # reads as count 0)
     per_frame = lambda n: 1000.0 * kt[n][0] / kt[n][1] if kt[n][1] > 0 else 0.0
@@ -464,8 +465,39 @@ def run_k5(a, ws, rank, dev):
            "copy_floor_ms": round(floor["ms"], 4),
            "copy_floor": floor,
            "frac_of_copy_floor": round(floor["ms"] / (1000.0 * elapsed / a.steps), 4),
+           "pose_vs_trace": vs_trace,
            "cpu_baseline": cpu}
     return out
+
+
+def k5_vs_trace(poses, frames, R, Cc, F, seed, warmup):
+    """The run's pose chain against the committed oracle trace of the same
+    stream (tests/golden/k5_trace.npz, make_k5_trace.py): every frame the
+    trace covers, warmup and timed alike (frame i's pose is poses[i - 1]).
+    None when this rank's stream is not the trace's."""
+    import hashlib
+    path = os.path.join(ROOT, "tests", "golden", "k5_trace.npz")
+    if not os.path.exists(path):
+        return None
+    with np.load(path) as z:
+        tr = {k: z[k] for k in z.files}
+    if (int(tr["R"]), int(tr["C"]), int(tr["F"]), int(tr["seed"])) != (R, Cc, F, seed):
+        return None
+    if hashlib.sha256(np.ascontiguousarray(frames, np.float64).tobytes()).hexdigest() != \
+            str(tr["frames_sha256"]):
+        return None
+    n = min(len(poses), len(tr["pose"]))
+    g, c = np.asarray(poses[:n]), tr["pose"][:n]
+    d = g[:, :3] - c[:, :3]
+    timed = slice(warmup, n)
+    return {"frames": n, "timed_frames": max(0, n - warmup),
+            "rmse_mm": float(np.sqrt(np.mean(np.sum(d * d, axis=1)))),
+            "rmse_mm_timed": (float(np.sqrt(np.mean(np.sum(d[timed] ** 2, axis=1))))
+                              if n > warmup else None),
+            "max_abs_mm_or_deg": float(np.max(np.abs(g - c))),
+            "bit_exact": bool(np.array_equal(g, c)),
+            "source": "tests/golden/k5_trace.npz (the pinned oracle's src/slam.c restatement, "
+                      f"{len(tr['pose'])} frames)"}
 
 
 def k5_copy_floor(L, ctx, pcs, attr, npts, reps=20):

@@ -1534,3 +1534,74 @@ def test_pair_knn_on_l9_scans_vs_oracle(kgpu, orc):
     ri, rd = _memo("pair_l9", lambda: orc.knn_grid(tgt, src, k))
     _eq(idx.cpu().numpy(), ri, "idx")
     _eq(dst.cpu().numpy(), rd, "dist")
+
+
+def _k5_trace():
+    """tests/golden/k5_trace.npz (make_k5_trace.py): the pinned oracle's pose
+    trace of the bench's K5 stream (rank 0: 128 x 2048, 8 frames, seed 11)."""
+    import os
+    path = os.path.join(os.path.dirname(__file__), "golden", "k5_trace.npz")
+    with np.load(path) as z:
+        return {k: z[k] for k in z.files}
+
+
+def _k5_run(monkeypatch, n, adam, trees="1"):
+    """The bench's K5 loop (bench.py run_k5, src/main.c:361-431) through the
+    drop-in shim for n frames: per-frame pose, error and correspondences."""
+    monkeypatch.setenv("NAVSLAM_QUIET", "1")
+    monkeypatch.setenv("NAVSLAM_HOST_TREES", trees)
+    if adam == "fast":
+        monkeypatch.setenv("NAVSLAM_ADAM", "fast")
+    else:
+        monkeypatch.delenv("NAVSLAM_ADAM", raising=False)
+    from shimlib import Pos, Shim
+    from navslam.synth import l9_stream, l9_stream_index
+    tr = _k5_trace()
+    R, Cc, F, seed = (int(tr[k]) for k in ("R", "C", "F", "seed"))
+    frames = l9_stream(R, Cc, F, seed=seed)
+    sh = Shim(R, Cc)
+    attr = sh.SLAMAttr()
+    pcs = [sh.cloud(frames[f], ts=f) for f in range(F)]
+    zero = Pos.of([0.0] * 6)
+    sh.L.init_slam(C.byref(attr), zero, C.byref(pcs[0]))
+    last = zero
+    pose, err, corr = [], [], []
+    for i in range(1, n + 1):
+        pc = pcs[l9_stream_index(i, F)]
+        meas = sh.L.slam_localization(C.byref(attr), C.byref(pc), last, last)
+        sh.L.slam_mapping(C.byref(attr), meas, C.byref(pc))
+        pose.append(meas.tolist())
+        err.append(attr.error)
+        corr.append(sh.last_frame_stats()[1])
+        last = meas
+    return tr, np.array(pose), np.array(err), np.array(corr)
+
+
+def test_k5_exact_stream_matches_trace_bit_exact(monkeypatch):
+    """K5 exact mode (the default: the reference's sequential dedup + Adam
+    sums on the host) over the first 50 frames of the bench's stream: every
+    pose, error and correspondence count bit-exact against the committed
+    oracle trace (host trees on)."""
+    tr, pose, err, corr = _k5_run(monkeypatch, 50, "exact")
+    _eq(pose, tr["pose"][:50], "K5 exact poses vs trace")
+    _eq(err, tr["error"][:50], "K5 exact errors vs trace")
+    _eq(corr, tr["corr"][:50], "K5 exact correspondences vs trace")
+
+
+@pytest.mark.parametrize("trees", ["1", "0"])
+def test_k5_fast_stream_vs_trace(monkeypatch, trees):
+    """K5 fast mode (GPU dedup + closed-form Adam sums, NAVSLAM_ADAM=fast)
+    running freely over 1,000 frames of the bench's stream (125 back-and-forth
+    passes over its 8 ray-cast frames): the pose chain against the committed
+    oracle trace. The order-free sums round differently from the reference's
+    sequential ones, so the bound is on the drift: translation
+    RMSE over all frames <= 1e-6 mm and every coordinate within 1e-5 (mm or
+    degrees); the correspondence count of every frame equal."""
+    n = 1000
+    tr, pose, err, corr = _k5_run(monkeypatch, n, "fast", trees)
+    ref = tr["pose"][:n]
+    d = pose[:, :3] - ref[:, :3]
+    rmse = float(np.sqrt(np.mean(np.sum(d * d, axis=1))))
+    assert rmse <= 1e-6, rmse
+    np.testing.assert_allclose(pose, ref, rtol=0, atol=1e-5)
+    _eq(corr, tr["corr"][:n], "K5 fast correspondences vs trace")
