@@ -1577,27 +1577,32 @@ def _k5_run(monkeypatch, n, adam, trees="1"):
     return tr, np.array(pose), np.array(err), np.array(corr)
 
 
-def test_k5_exact_stream_matches_trace_bit_exact(monkeypatch):
+@pytest.mark.parametrize("trees", ["1", "0"])
+def test_k5_exact_stream_matches_trace_bit_exact(monkeypatch, trees):
     """K5 exact mode (the default: the reference's sequential dedup + Adam
-    sums on the host) over the first 50 frames of the bench's stream: every
-    pose, error and correspondence count bit-exact against the committed
-    oracle trace (host trees on)."""
-    tr, pose, err, corr = _k5_run(monkeypatch, 50, "exact")
-    _eq(pose, tr["pose"][:50], "K5 exact poses vs trace")
-    _eq(err, tr["error"][:50], "K5 exact errors vs trace")
-    _eq(corr, tr["corr"][:50], "K5 exact correspondences vs trace")
+    sums on the host, ~30 ms per frame) over the first 200 frames of the
+    bench's stream (25 back-and-forth passes over its 8 frames, the map ring
+    wrapped twice): every pose, error and correspondence count bit-exact
+    against the committed oracle trace, host trees on and off (lazy rows)."""
+    n = 200
+    tr, pose, err, corr = _k5_run(monkeypatch, n, "exact", trees)
+    _eq(pose, tr["pose"][:n], "K5 exact poses vs trace")
+    _eq(err, tr["error"][:n], "K5 exact errors vs trace")
+    _eq(corr, tr["corr"][:n], "K5 exact correspondences vs trace")
 
 
 @pytest.mark.parametrize("trees", ["1", "0"])
 def test_k5_fast_stream_vs_trace(monkeypatch, trees):
     """K5 fast mode (GPU dedup + closed-form Adam sums, NAVSLAM_ADAM=fast)
-    running freely over 1,000 frames of the bench's stream (125 back-and-forth
-    passes over its 8 ray-cast frames): the pose chain against the committed
-    oracle trace. The order-free sums round differently from the reference's
-    sequential ones, so the bound is on the drift: translation
-    RMSE over all frames <= 1e-6 mm and every coordinate within 1e-5 (mm or
-    degrees); the correspondence count of every frame equal."""
-    n = 1000
+    running freely over the whole configured stream, every frame the trace
+    holds (10,000: BASELINE.json configs[4]; 714 back-and-forth passes over
+    the 8 ray-cast frames, under a millisecond each): the pose chain against
+    the committed oracle trace. The order-free sums round differently from
+    the reference's sequential ones, so the bound is on the
+    drift: translation RMSE over all frames <= 1e-6 mm and every coordinate
+    within 1e-5 (mm or degrees); the correspondence count of every frame
+    equal."""
+    n = len(_k5_trace()["pose"])
     tr, pose, err, corr = _k5_run(monkeypatch, n, "fast", trees)
     ref = tr["pose"][:n]
     d = pose[:, :3] - ref[:, :3]
