@@ -1,4 +1,4 @@
-export NAVSLAM_QUIET=1; OUT=gpurun_out/r6k; mkdir -p $OUT
-timeout -k 10 600 python3 -u -m pytest tests -m gpu -x -v --timeout 400 --timeout-method thread -k "k5_" > $OUT/pytest.log 2>&1; rc=$?; echo pytest rc=$rc; grep -E "PASSED|FAILED|Error|assert" $OUT/pytest.log | head -20; [ $rc -ne 0 ] && exit $rc
-NAVSLAM_HOST_TREES=0 timeout -k 10 400 python3 bench.py --workload k5 --k5-mode fast --steps 300 --warmup 10 --no-traffic-json --json-out $OUT/bench_k5_fast_lazy.json > $OUT/bench_k5.log 2>&1; echo bench rc=$?
-python3 -c "import json; d=json.load(open('$OUT/bench_k5_fast_lazy.json')); print(d['ms_per_step'], d['pose_vs_trace'], d['cpu_baseline'] and d['cpu_baseline'].get('pose_rmse_mm'))"
+export NAVSLAM_QUIET=1
+timeout -k 10 600 python3 -u -m pytest tests -m gpu -x -q --timeout 240 --timeout-method thread -k "knn" > gpurun_out/r6m_pytest.log 2>&1; rc=$?; echo pytest rc=$rc; tail -2 gpurun_out/r6m_pytest.log; [ $rc -ne 0 ] && exit $rc
+bash scripts/r6_trace_ab.sh r6m nb2: nb1:nav-slam_amd/lib/variants/libnavgpu_nb1.so nb2b: nb1b:nav-slam_amd/lib/variants/libnavgpu_nb1.so
+bash scripts/r6_ab.sh r6m 2 "nb2:NAVGPU_KNN_MODE=2" "nb1:NAVGPU_LIB=nav-slam_amd/lib/variants/libnavgpu_nb1.so"
