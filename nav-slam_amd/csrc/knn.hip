@@ -144,16 +144,29 @@ struct GridArgs {
 // at `cap` cells; the tile width of k_knn. Run by a whole 256-thread block
 // (every k_bin_hist block derives its own copy: one launch fewer than a
 // separate grid kernel); thread 0 writes *out.
-__device__ void grid_params_block(const GridArgs A, GridParams *out) {
-  const double *part = A.part;
-  const int nparts = A.nparts, cap = A.cap, sx = A.sx;
+// this thread's share of the bbox partials (loaded first, so that a caller
+// can issue other loads behind them and still wait for these alone)
+struct Part6 {
+  double v[6];
+};
+// One partial per thread at most (nparts <= kBBoxBlocks <= the block size):
+// loaded unconditionally from a clamped slot, masked only when used.
+__device__ __forceinline__ Part6 grid_partials(const GridArgs A) {
+  Part6 P;
+  const double *q = A.part + 6 * min((int)threadIdx.x, max(A.nparts - 1, 0));
+#pragma unroll
+  for (int a = 0; a < 6; ++a) P.v[a] = q[a];
+  return P;
+}
+__device__ void grid_params_block(const GridArgs A, GridParams *out, const Part6 &P) {
+  const int cap = A.cap, sx = A.sx;
   const double occ = A.occ;
   const size_t n = A.n;
   __shared__ double s[16][6];  // one row per wave (<= 1024 threads)
-  double v6[6] = {INFINITY, INFINITY, INFINITY, -INFINITY, -INFINITY, -INFINITY};
-  for (int b = threadIdx.x; b < nparts; b += blockDim.x)
-    for (int a = 0; a < 6; ++a)
-      v6[a] = a < 3 ? fmin(v6[a], part[b * 6 + a]) : fmax(v6[a], part[b * 6 + a]);
+  double v6[6];
+  const bool has = (int)threadIdx.x < A.nparts;  // (a select, not a branch: the
+  for (int a = 0; a < 6; ++a)                     // wait stays behind the points)
+    v6[a] = has ? P.v[a] : (a < 3 ? INFINITY : -INFINITY);
 #pragma unroll
   for (int a = 0; a < 3; ++a)
     for (int o = kWave / 2; o > 0; o >>= 1) {
@@ -445,22 +458,39 @@ __device__ __forceinline__ int bin_side(const BinJob &J, int &blk) {
 struct P3 {
   double x, y, z;
 };
+#ifndef NAVGPU_BIN_PRELOAD
+#define NAVGPU_BIN_PRELOAD 1  // (r6) the first batch's point loads before the block's setup
+#endif
+constexpr bool kBinPreload = NAVGPU_BIN_PRELOAD;
 
 // the block's chunk in batches of kBinUnroll points per thread: every load of
-// a batch is issued before any of its cells is used
-template <class F>
-__device__ __forceinline__ void bin_chunk(const BinSide &S, int blk, const GridParams &G, F f) {
+// a batch is issued before any of its cells is used. `prep` runs once, after
+// the first batch's loads are issued and before any is used, and returns the
+// grid (r6: the block's setup -- deriving the grid, scanning the bucket
+// bases -- then overlaps the first round trip to HBM instead of preceding it)
+// (`fallback`: any 24 readable device bytes, the source of an empty chunk's
+// first loads, which are issued unconditionally so that no branch makes the
+// compiler's wait counts conservative)
+template <class Prep, class F>
+__device__ __forceinline__ void bin_chunk(const BinSide &S, int blk, const void *fallback,
+                                          Prep prep, F f) {
   const int i0 = blk * S.P, i1 = min(S.n, (blk + 1) * S.P);
   const int bd = (int)blockDim.x;
-  for (int ib = i0; ib < i1; ib += kBinUnroll * bd) {
-    P3 v[kBinUnroll];
+  const double *src = i1 > i0 ? S.p : (const double *)fallback;
+  P3 v[kBinUnroll];
+  auto load = [&](int ib) {
     // every load issued unconditionally from a clamped index (r5, as in
     // k_bbox_partial); the lanes past the chunk drop theirs below
 #pragma unroll
     for (int u = 0; u < kBinUnroll; ++u) {
       const int i = ib + u * bd + (int)threadIdx.x;
-      v[u] = *(const P3 *)(S.p + 3 * (size_t)min(i, i1 - 1));
+      v[u] = *(const P3 *)(src + 3 * (size_t)max(min(i, i1 - 1), 0));
     }
+  };
+  if (kBinPreload) load(i0);
+  const GridParams G = prep();
+  for (int ib = i0; ib < i1; ib += kBinUnroll * bd) {
+    if (!kBinPreload || ib != i0) load(ib);
 #pragma unroll
     for (int u = 0; u < kBinUnroll; ++u) {
       const int i = ib + u * bd + (int)threadIdx.x;
@@ -476,6 +506,7 @@ __device__ __forceinline__ void bin_chunk(const BinSide &S, int blk, const GridP
 #define NAVGPU_BIN_THREADS 512  // (r6 A/B: k_bin_scatter 25.9 -> 23.9 us against 256; 1024: k_bin_hist 14.8 -> 22)
 #endif
 constexpr int kBinThreads = NAVGPU_BIN_THREADS;  // threads per k_bin_hist / k_bin_scatter block
+static_assert(kBBoxBlocks <= kBinThreads, "grid_partials: one bbox partial per thread");
 __global__ __launch_bounds__(kBinThreads, kBuildMinW) void k_bin_hist(BinJob J, const GridArgs A,
                                                   GridParams *__restrict__ gp,
                                                   int *__restrict__ counters,
@@ -485,15 +516,21 @@ __global__ __launch_bounds__(kBinThreads, kBuildMinW) void k_bin_hist(BinJob J, 
   int blk = blockIdx.x;
   const BinSide S = J.s[bin_side(J, blk)];
   for (int b = threadIdx.x; b < J.nb; b += blockDim.x) hist[b] = 0;
-  grid_params_block(A, &sG);
-  if (blockIdx.x == 0 && threadIdx.x < 16) counters[threadIdx.x] = 0;  // [4, 12): tickets
-  __syncthreads();
-  const GridParams G = sG;  // (by value: registers, not an LDS read per point)
-  if (blockIdx.x == 0 && threadIdx.x == 0) *gp = G;
-  bin_chunk(S, blk, G, [&](int i, const P3 &, int c) {
-    atomicAdd(&hist[c >> J.shift], 1);
-    if (S.rawcell) S.rawcell[i] = c;
-  });
+  const Part6 P = grid_partials(A);  // (issued before the points: waited for alone)
+  bin_chunk(
+      S, blk, A.part,
+      [&]() {
+        grid_params_block(A, &sG, P);
+        if (blockIdx.x == 0 && threadIdx.x < 16) counters[threadIdx.x] = 0;  // [4, 12): tickets
+        __syncthreads();
+        const GridParams G = sG;  // (by value: registers, not an LDS read per point)
+        if (blockIdx.x == 0 && threadIdx.x == 0) *gp = G;
+        return G;
+      },
+      [&](int i, const P3 &, int c) {
+        atomicAdd(&hist[c >> J.shift], 1);
+        if (S.rawcell) S.rawcell[i] = c;
+      });
   __syncthreads();
   for (int b = threadIdx.x; b < J.nb; b += blockDim.x) table[S.tab + blk * J.nb + b] = hist[b];
 }
@@ -507,9 +544,9 @@ __global__ __launch_bounds__(kBinThreads, kBuildMinW) void k_bin_scatter(BinJob 
   int blk = blockIdx.x;
   const int side = bin_side(J, blk);
   const BinSide S = J.s[side];
-  const GridParams G = *gp;
-  // the side's bucket bases: exclusive scan of btot, each thread a run
-  {
+  // the side's bucket bases: exclusive scan of btot, each thread a run (run
+  // once the block's first batch of points or cells is in flight)
+  auto bases = [&]() {
     const int *bt = btot + side * J.nb;
     const int per = (J.nb + blockDim.x - 1) / blockDim.x;
     const int j0 = min(J.nb, (int)threadIdx.x * per), j1 = min(J.nb, j0 + per);
@@ -526,18 +563,23 @@ __global__ __launch_bounds__(kBinThreads, kBuildMinW) void k_bin_scatter(BinJob 
       acc += v;
     }
     if (bo && threadIdx.x == 0) bo[J.nb] = total;
-  }
-  __syncthreads();
+    __syncthreads();
+  };
   if (side) {  // queries: their cells as k_bin_hist kept them
     const int i0 = blk * S.P, i1 = min(S.n, (blk + 1) * S.P);
     const int bd = (int)blockDim.x;
-    for (int ib = i0; ib < i1; ib += kBinUnroll * bd) {
-      int c[kBinUnroll];
+    int c[kBinUnroll];
+    auto load = [&](int ib) {
 #pragma unroll
       for (int u = 0; u < kBinUnroll; ++u) {
         const int i = ib + u * bd + (int)threadIdx.x;
-        c[u] = S.rawcell[min(i, i1 - 1)];  // (clamped, unconditional; dropped below)
+        c[u] = S.rawcell[max(min(i, i1 - 1), 0)];  // (clamped, unconditional; dropped below)
       }
+    };
+    if (kBinPreload) load(i0);  // (an empty chunk reads its clamped slot 0: nq > 0 here)
+    bases();
+    for (int ib = i0; ib < i1; ib += kBinUnroll * bd) {
+      if (!kBinPreload || ib != i0) load(ib);
 #pragma unroll
       for (int u = 0; u < kBinUnroll; ++u) {
         const int i = ib + u * bd + (int)threadIdx.x;
@@ -546,18 +588,22 @@ __global__ __launch_bounds__(kBinThreads, kBuildMinW) void k_bin_scatter(BinJob 
     }
     return;
   }
-  bin_chunk(S, blk, G, [&](int i, const P3 &v, int c) {
-    const int pos = atomicAdd(&cur[c >> J.shift], 1);
-    {
-      BinPt t;
-      t.x = v.x;
-      t.y = v.y;
-      t.z = v.z;
-      t.idx = i;
-      t.cell = c;
-      S.bin[pos] = t;
-    }
-  });
+  bin_chunk(
+      S, blk, gp,
+      [&]() {
+        bases();
+        return *gp;
+      },
+      [&](int i, const P3 &v, int c) {
+        const int pos = atomicAdd(&cur[c >> J.shift], 1);
+        BinPt t;
+        t.x = v.x;
+        t.y = v.y;
+        t.z = v.z;
+        t.idx = i;
+        t.cell = c;
+        S.bin[pos] = t;
+      });
 }
 
 // One bucket: count its points per cell (LDS), scan, write the cell starts,
