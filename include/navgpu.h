@@ -318,6 +318,13 @@ int navgpu_knn_check(navgpu_ctx *ctx);
  * with a distance tie and so ran the reference tree (synchronises); -1 when
  * the last call did not screen (NAVGPU_ROWS_SCREEN=0) or none was made. */
 long long navgpu_rows_tie_rows(navgpu_ctx *ctx);
+/* Diagnostic: one reference nth_element (utils/kdtree.c:20-52: Lomuto,
+ * pivot = last, `<= 0` goes left) over keys[perm[first..last]] as the
+ * per-row builds run it (block = 0: one wave, its ordinary and register
+ * passes; 1: the 1024-thread block pass), permuting the device
+ * array perm (values < n, n <= 8191) in place; asynchronous on the stream. */
+int navgpu_debug_nth_element(navgpu_ctx *ctx, const double *key, int32_t *perm, int n,
+                             int first, int last, int nth, int block);
 
 #ifdef __cplusplus
 }

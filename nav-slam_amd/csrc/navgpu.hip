@@ -2254,6 +2254,29 @@ __global__ __launch_bounds__(kRowsBlock) void k_rows_retree(
 
 // ---------------------------------------- R5 for one arbitrary array
 // kdtree.h buildKDTree: n points, in place, root axis depth0 % 3.
+// Diagnostic (r6): one reference nth_element (utils/kdtree.c:20-52) as the
+// per-row builds run it, by one wave (wave_nth_element: ordinary and register
+// passes) or by the block (block_nth_element), on keys and a
+// permutation of n <= kMaxRowCols positions (navgpu_debug_nth_element)
+__global__ __launch_bounds__(1024) void k_debug_nth(const double *__restrict__ key,
+                                                    int32_t *__restrict__ perm, int n, int first,
+                                                    int last, int nth, int block) {
+  double *K = (double *)smem;
+  uint16_t *P = (uint16_t *)(smem + align16(8 * n));
+  uint16_t *T = P + align16(2 * n) / 2;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) {
+    K[i] = key[i];
+    P[i] = (uint16_t)perm[i];
+  }
+  __syncthreads();
+  if (block)
+    block_nth_element<uint16_t>(K, P, T, first, last, nth);
+  else if (threadIdx.x < kWave)
+    wave_nth_element<uint16_t>(K, P, T, first, last, nth, (int)threadIdx.x);
+  __syncthreads();
+  for (int i = threadIdx.x; i < n; i += blockDim.x) perm[i] = P[i];
+}
+
 __global__ __launch_bounds__(1024) void k_kd_build_lds(double *__restrict__ pts,
                                                        int n, int depth0) {
   double *FC = (double *)smem;
@@ -3073,6 +3096,18 @@ int navgpu_debug_stamps(unsigned long long *out16) {
   (void)out16;
   return NAVGPU_EINVAL;
 #endif
+}
+
+int navgpu_debug_nth_element(navgpu_ctx *ctx, const double *key, int32_t *perm, int n,
+                             int first, int last, int nth, int block) {
+  ARG_CHECK(ctx && key && perm);
+  ARG_CHECK(n >= 1 && n <= kMaxRowCols && 0 <= first && first <= nth && nth <= last && last < n);
+  const int lds = align16(8 * n) + 2 * align16(2 * n);
+  RC(set_lds(k_debug_nth, lds));
+  hipLaunchKernelGGL(k_debug_nth, dim3(1), dim3(block ? 1024 : kWave), lds, ctx->stream, key,
+                     perm, n, first, last, nth, block ? 1 : 0);
+  CHECK_LAUNCH("k_debug_nth");
+  return NAVGPU_OK;
 }
 
 long long navgpu_rows_tie_rows(navgpu_ctx *ctx) {

@@ -89,6 +89,8 @@ def _declare(L):
         "navgpu_knn_overflows": (C.c_longlong, [_vp]),
         "navgpu_knn_check": (C.c_int, [_vp]),
         "navgpu_rows_tie_rows": (C.c_longlong, [_vp]),
+        "navgpu_debug_nth_element": (C.c_int, [_vp, _vp, _vp, C.c_int, C.c_int, C.c_int,
+                                               C.c_int, C.c_int]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -204,6 +206,13 @@ class NavGpu:
         """Rows of the last rows_match call that had a distance tie and ran
         the reference tree (-1 if that call did not screen)."""
         return self.L.navgpu_rows_tie_rows(self.h)
+
+    def debug_nth_element(self, key, perm, first, last, nth, block=False):
+        """One reference nth_element as the per-row builds run it (device
+        tensors: key f64 [n], perm int32 [n], permuted in place)."""
+        self._check(self.L.navgpu_debug_nth_element(self.h, _ptr(key), _ptr(perm), len(perm),
+                                                    first, last, nth, 1 if block else 0),
+                    "debug_nth_element")
 
     def timing_read(self, name, reset=True):
         n = self.L.navgpu_timing_count(self.h, name.encode())

@@ -39,6 +39,7 @@ class Oracle:
         L.orc_rotation_matrix_deg.argtypes = [C.c_double] * 3 + [_dp]
         L.orc_transform_cloud.argtypes = [_dp, C.c_size_t, _dp, _dp, _dp]
         L.orc_kd_build.argtypes = [_dp, _ip, C.c_size_t]
+        L.orc_nth_element.argtypes = [_dp, _ip, C.c_size_t, C.c_size_t, C.c_size_t, C.c_int]
         L.orc_kd_nn.argtypes = [_dp, C.c_size_t, _dp, C.POINTER(C.c_long), _dp]
         L.orc_rows_match.argtypes = [_dp, _dp, C.c_int, C.c_int, _ip, _ip, _ip, _dp]
         L.orc_knn_brute.argtypes = [_dp, C.c_size_t, _dp, C.c_size_t, C.c_int, _ip, _dp]
@@ -102,6 +103,16 @@ class Oracle:
         out = np.zeros_like(pts)
         self.L.orc_transform_cloud(_d(pts), pts.size // 3, _d(Rm), _d(t), _d(out))
         return out
+
+    def nth_element(self, key, perm, first, last, nth):
+        """utils/kdtree.c:20-52 on keys[perm[first..last]] (axis 0): returns
+        the permutation after the reference's Lomuto quickselect."""
+        key = np.asarray(key, np.float64)
+        ix = np.ascontiguousarray(perm, np.int32).copy()
+        p = np.zeros((len(ix), 3))
+        p[:, 0] = key[ix]
+        self.L.orc_nth_element(_d(p), _i(ix), first, last, nth, 0)
+        return ix
 
     def kd_build(self, pts):
         """Returns (permuted points, permutation of original indices)."""

@@ -192,6 +192,43 @@ def test_kd_build_level_parallel_equals_single_workgroup(gpu, monkeypatch):
     _eq(a, b, "level-parallel vs single-workgroup build")
 
 
+
+@pytest.mark.parametrize("kind", ["random", "scanlike", "duplicates", "nonfinite"])
+def test_nth_element_matches_reference(gpu, orc, kind):
+    """The per-row builds' nth_element (one wave: ordinary passes over
+    64-position chunks and the register-resident pass; the 1024-thread block
+    pass with its hand-over to wave 0) against the oracle's
+    utils/kdtree.c:20-52 on windows of 2..4000 positions at any offset,
+    scan-like keys (long left-descent chains) and non-finite keys included."""
+    import torch
+    dev = torch.device("cuda", 0)
+    rng = np.random.default_rng(len(kind) + 40)
+    for trial in range(40):
+        n = int(rng.integers(2, 4000)) if trial % 3 else int(rng.integers(2, 300))
+        if kind == "scanlike":
+            key = np.cumsum(rng.normal(-0.3, 1.0, n))
+        elif kind == "duplicates":
+            key = np.round(rng.uniform(0, 6, n))
+        else:
+            key = rng.uniform(-1, 1, n)
+        if kind == "nonfinite":
+            for v in (np.inf, -np.inf, np.nan, 0.0, -0.0):
+                key[rng.integers(0, n, 3)] = v
+        perm = rng.permutation(n).astype(np.int32)
+        first = int(rng.integers(0, n))
+        last = int(rng.integers(first, n))
+        nth = int(rng.integers(first, last + 1))
+        ref = orc.nth_element(key, perm, first, last, nth)
+        for block in (False, True):
+            kd = torch.tensor(key, dtype=torch.float64, device=dev)
+            pd = torch.tensor(perm, dtype=torch.int32, device=dev)
+            gpu.debug_nth_element(kd, pd, first, last, nth, block=block)
+            torch.cuda.synchronize()
+            np.testing.assert_array_equal(pd.cpu().numpy(), ref,
+                                          err_msg=f"{kind} n={n} [{first},{last}] nth={nth} "
+                                                  f"block={block}")
+
+
 # ------------------------------------------------------ R4-R6 per-row mode
 def test_rows_match_l9_golden(gpu, golden):
     g = golden("rows_l9")
