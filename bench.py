@@ -1013,12 +1013,15 @@ TRAFFIC_SETS = {"k3": (QUERY_KERNELS, QUERY_MAIN), "k3_build": (BUILD_KERNELS, Q
 
 def traffic_tag(a):
     """profiles/traffic_<tag>.json: the PMC bytes a bench line of this
-    workload quotes (k3, k2, k2i, k4, k4i, k5, k5f)."""
+    workload quotes (k3, k2, k2i, k4, k4i, k5, k5f, k5fl: fast mode with lazy
+    row trees, NAVSLAM_HOST_TREES=0)."""
     t = a.workload
     if a.workload in ("k2", "k4") and a.integer_mm:
         t += "i"
     if a.workload == "k5" and a.k5_mode == "fast":
         t += "f"
+        if os.environ.get("NAVSLAM_HOST_TREES", "1") == "0":
+            t += "l"
     return t
 
 

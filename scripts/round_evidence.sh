@@ -61,6 +61,7 @@ pmc k2i --points 262144 --pairs 1 -- --workload k2 --integer-mm --steps 10
 pmc k4 --points 262144 --pairs 256 -- --workload k4 --steps 2 --warmup 1
 pmc k4i --points 262144 --pairs 256 -- --workload k4 --integer-mm --steps 2 --warmup 1
 pmc k5f --points 262144 -- --workload k5 --k5-mode fast --steps 20 --warmup 2
+NAVSLAM_HOST_TREES=0 pmc k5fl --points 262144 -- --workload k5 --k5-mode fast --steps 20 --warmup 2
 fi
 if part bench; then
 # a traffic json made earlier in this session, else the committed one
@@ -73,8 +74,8 @@ step bench_k4 400 python3 bench.py --workload k4 --steps 3 --warmup 1 --traffic-
 step bench_k4i 400 python3 bench.py --workload k4 --integer-mm --steps 3 --warmup 1 --traffic-json "$(tj k4i)" --json-out "$OUT/bench_k4i.json"
 step bench_k5 400 python3 bench.py --workload k5 --steps 30 --warmup 2 --json-out "$OUT/bench_k5.json"
 step bench_k5_fast 400 python3 bench.py --workload k5 --k5-mode fast --steps 30 --warmup 2 --traffic-json "$(tj k5f)" --json-out "$OUT/bench_k5_fast.json"
-NAVSLAM_HOST_TREES=0 step bench_k5_fast_lazy 400 python3 bench.py --workload k5 --k5-mode fast --steps 300 --warmup 10 --no-traffic-json --json-out "$OUT/bench_k5_fast_lazy.json"
-NAVSLAM_HOST_TREES=0 step bench_k5_fast_lazy_10k 600 python3 bench.py --workload k5 --k5-mode fast --steps 9990 --warmup 10 --no-traffic-json --no-cpu-baseline --json-out "$OUT/bench_k5_fast_lazy_10k.json"
+NAVSLAM_HOST_TREES=0 step bench_k5_fast_lazy 400 python3 bench.py --workload k5 --k5-mode fast --steps 300 --warmup 10 --traffic-json "$(tj k5fl)" --json-out "$OUT/bench_k5_fast_lazy.json"
+NAVSLAM_HOST_TREES=0 step bench_k5_fast_lazy_10k 600 python3 bench.py --workload k5 --k5-mode fast --steps 9990 --warmup 10 --traffic-json "$(tj k5fl)" --no-cpu-baseline --json-out "$OUT/bench_k5_fast_lazy_10k.json"
 step trace_k5 400 rocprofv3 --kernel-trace --stats -d "$OUT/trace_k5" -o run --output-format csv -- python3 bench.py --workload k5 --k5-mode fast --steps 20 --warmup 2 --no-cpu-baseline --no-traffic-json
 fi
 echo done

@@ -3,7 +3,7 @@ bench.py run -> profiles/traffic_<tag>.json, which bench.py quotes as
 roofline.traffic (and, for K3, roofline.build.traffic): the counters cannot
 run inside the timed bench.
 
-usage: traffic_json.py FETCH_CSV WRITE_CSV OUT ROUND_TAG [--workload k3|k2|k2i|k4|k4i|k5|k5f]
+usage: traffic_json.py FETCH_CSV WRITE_CSV OUT ROUND_TAG [--workload k3|k2|k2i|k4|k4i|k5|k5f|k5fl]
                        [--points N] [--pairs P] [--k K] [--src "command"]
 """
 import argparse
