@@ -46,8 +46,13 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (8.0 TB/s spec)
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=20)
-    p.add_argument("--warmup", type=int, default=3)
+    # (r6: 200 timed steps by default. With pairs in flight the timed region
+    # starts on an empty pipeline and ends draining it; over 20 steps that
+    # and the first steps' cold clocks cost the K3 line ~9 % (0.2386-0.2427
+    # vs 0.2197-0.2206 ms per pair at 200, profiles/r6/k3_steps_ab.txt); a
+    # K3 step is ~0.22 ms, the slowest default line (K4i) ~6 s)
+    p.add_argument("--steps", type=int, default=200)
+    p.add_argument("--warmup", type=int, default=10)
     p.add_argument("--workload", choices=["k3", "k2", "k4", "k5"], default="k3")
     p.add_argument("--stream-frames", type=int, default=8,
                    help="k5: distinct ray-cast frames, replayed back and forth")
