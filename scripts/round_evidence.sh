@@ -68,10 +68,10 @@ if part bench; then
 tj() { if [ -f "$OUT/traffic_$1.json" ]; then echo "$OUT/traffic_$1.json"; else echo "profiles/traffic_$1.json"; fi; }
 step bench_k3 600 python3 bench.py --traffic-json "$(tj k3)" --json-out "$OUT/bench_k3.json"
 step bench_k3_inflight1 300 python3 bench.py --inflight 1 --no-cpu-baseline --traffic-json "$(tj k3)" --json-out "$OUT/bench_k3_inflight1.json"
-step bench_k2 300 python3 bench.py --workload k2 --steps 10 --traffic-json "$(tj k2)" --json-out "$OUT/bench_k2.json"
-step bench_k2i 300 python3 bench.py --workload k2 --integer-mm --steps 10 --traffic-json "$(tj k2i)" --json-out "$OUT/bench_k2i.json"
-step bench_k4 400 python3 bench.py --workload k4 --steps 3 --warmup 1 --traffic-json "$(tj k4)" --json-out "$OUT/bench_k4.json"
-step bench_k4i 400 python3 bench.py --workload k4 --integer-mm --steps 3 --warmup 1 --traffic-json "$(tj k4i)" --json-out "$OUT/bench_k4i.json"
+step bench_k2 300 python3 bench.py --workload k2 --steps 100 --traffic-json "$(tj k2)" --json-out "$OUT/bench_k2.json"
+step bench_k2i 300 python3 bench.py --workload k2 --integer-mm --steps 100 --traffic-json "$(tj k2i)" --json-out "$OUT/bench_k2i.json"
+step bench_k4 400 python3 bench.py --workload k4 --steps 10 --warmup 2 --traffic-json "$(tj k4)" --json-out "$OUT/bench_k4.json"
+step bench_k4i 400 python3 bench.py --workload k4 --integer-mm --steps 10 --warmup 2 --traffic-json "$(tj k4i)" --json-out "$OUT/bench_k4i.json"
 step bench_k5 400 python3 bench.py --workload k5 --steps 30 --warmup 2 --json-out "$OUT/bench_k5.json"
 step bench_k5_fast 400 python3 bench.py --workload k5 --k5-mode fast --steps 30 --warmup 2 --traffic-json "$(tj k5f)" --json-out "$OUT/bench_k5_fast.json"
 NAVSLAM_HOST_TREES=0 step bench_k5_fast_lazy 400 python3 bench.py --workload k5 --k5-mode fast --steps 300 --warmup 10 --traffic-json "$(tj k5fl)" --json-out "$OUT/bench_k5_fast_lazy.json"
