@@ -81,7 +81,7 @@ constexpr int kBBoxBlocks = 256;  // bbox partials (every k_bin_hist block reduc
 #define NAVGPU_BBOX_U 4
 #endif
 #ifndef NAVGPU_BBOX_THREADS
-#define NAVGPU_BBOX_THREADS 256
+#define NAVGPU_BBOX_THREADS 512  // (r6, 200-step bench A/B: 6 of 7 interleaved rounds faster than 256, ~1 %)
 #endif
 constexpr int kBBoxThreads = NAVGPU_BBOX_THREADS;  // threads per k_bbox_partial block
 static_assert(kBBoxThreads % kWave == 0 && kBBoxThreads <= 1024, "bbox block");
