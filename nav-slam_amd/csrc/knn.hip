@@ -433,7 +433,10 @@ __device__ __forceinline__ F3 make_f3(const GridParams &G, double x, double y, d
   return F3{(float)(x - G.c[0]), (float)(y - G.c[1]), (float)(z - G.c[2])};
 }
 constexpr int kBinMaxShift = 15;
-constexpr int kBinUnroll = kLean ? 4 : 8;  // points per thread with loads in flight
+#ifndef NAVGPU_BIN_UNROLL
+#define NAVGPU_BIN_UNROLL (NAVGPU_BUILD_LEAN ? 4 : 8)
+#endif
+constexpr int kBinUnroll = NAVGPU_BIN_UNROLL;  // points per thread with loads in flight
 // (compile-time knobs for A/B variant builds, scripts/build_variants.sh)
 #ifndef NAVGPU_BIN_P
 #define NAVGPU_BIN_P 4096
@@ -822,7 +825,10 @@ __device__ __forceinline__ int nb_pos(int yy, int zz, int x, int g0, int g1, int
 // 64 columns ~15 positions apart. (r5: writing each task's positions 64 at a
 // time, coalesced, through LDS run marks and a running max measured 33 against
 // 25 us: the marks' 32 KB per workgroup cost residency.)
-constexpr int kNbWaves = 4;  // waves per k_nb_fill workgroup
+#ifndef NAVGPU_NB_WAVES
+#define NAVGPU_NB_WAVES 4
+#endif
+constexpr int kNbWaves = NAVGPU_NB_WAVES;  // waves per k_nb_fill workgroup
 __global__ __launch_bounds__(kWave * kNbWaves) void k_nb_fill(const GridParams *__restrict__ gp,
                                                               const int *__restrict__ tstart,
                                                               int *__restrict__ npg,
