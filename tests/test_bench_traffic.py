@@ -73,11 +73,20 @@ def test_traffic_json_script_and_lookup(tmp_path):
     assert bench.load_traffic(a, {"k": 8}) is None
 
 
-def test_traffic_tags():
+def test_traffic_tags(monkeypatch):
     ns = lambda **kw: argparse.Namespace(**dict(dict(integer_mm=False, k5_mode="exact"), **kw))
     assert bench.traffic_tag(ns(workload="k2", integer_mm=True)) == "k2i"
     assert bench.traffic_tag(ns(workload="k4")) == "k4"
+    monkeypatch.delenv("NAVSLAM_HOST_TREES", raising=False)
     assert bench.traffic_tag(ns(workload="k5", k5_mode="fast")) == "k5f"
+    # fast mode with lazy row trees quotes its own PMC bytes (r6)
+    monkeypatch.setenv("NAVSLAM_HOST_TREES", "0")
+    assert bench.traffic_tag(ns(workload="k5", k5_mode="fast")) == "k5fl"
+    assert bench.traffic_tag(ns(workload="k5")) == "k5"
+    with open(os.path.join(ROOT, "profiles", "traffic_k5fl.json")) as fh:
+        tl = json.load(fh)
+    assert tl["workload"] == "k5fl" and tl["points_per_cloud"] == 128 * 2048
+    assert tl["bytes_per_step"] > 0
     # the default bench line reads the committed K3 json, which must match its config
     with open(os.path.join(ROOT, "profiles", "traffic_k3.json")) as fh:
         tj = json.load(fh)
