@@ -36,6 +36,13 @@ namespace {
 
 
 constexpr int kRowsBlock = 512;     // 8 waves per row workgroup
+#ifndef NAVGPU_ROWS_MATCH_BLOCK
+#define NAVGPU_ROWS_MATCH_BLOCK 1024  // (r6: K2i 0.716 -> 0.696 ms against 512, three interleaved rounds)
+#endif
+// k_rows_match's threads (the tie pass): the build by all of them, the walk
+// by the first kRowsBlock (their stacks are what rows_lds sizes)
+constexpr int kRowsMatchBlock = NAVGPU_ROWS_MATCH_BLOCK;
+static_assert(kRowsMatchBlock >= kRowsBlock && kRowsMatchBlock <= 1024, "rows match block");
 #ifndef NAVGPU_ROWS_BUILD_BLOCK
 #define NAVGPU_ROWS_BUILD_BLOCK 512
 #endif
@@ -913,7 +920,7 @@ __device__ __forceinline__ int canon_col(const double *TX, const double *TY, con
   return best;
 }
 
-__global__ __launch_bounds__(kRowsBlock) void k_rows_match(
+__global__ __launch_bounds__(kRowsMatchBlock) void k_rows_match(
     const double *__restrict__ src, const double *__restrict__ tgt, int R,
     int C, int32_t *__restrict__ src_mask, int32_t *__restrict__ tgt_mask,
     int32_t *__restrict__ nn_idx, double *__restrict__ nn_dist,
@@ -963,13 +970,13 @@ __global__ __launch_bounds__(kRowsBlock) void k_rows_match(
   const int nq = block_compact(
       C, scan, [&](int j) { return SM[j] != 0; },
       [&](int j, int pos) { QL[pos] = (uint16_t)j; });
-  for (int i = threadIdx.x; i < nq; i += blockDim.x) {
+  for (int i = threadIdx.x; (int)threadIdx.x < kRowsBlock && i < nq; i += kRowsBlock) {
     const int c = QL[i];
     int bpos;
     double bd;
     // a tied query's exact minimum came from the screen (-1: walk it all)
     kd_query(TX, TY, TZ, n, sraw[3 * c], sraw[3 * c + 1], sraw[3 * c + 2],
-             stk + threadIdx.x, blockDim.x, &bpos, &bd, tie ? nn_dist[rowoff + c] : -1.0);
+             stk + threadIdx.x, kRowsBlock, &bpos, &bd, tie ? nn_dist[rowoff + c] : -1.0);
     nn_idx[rowoff + c] = bpos >= 0 ? pair_row0 + canon_col(TX, TY, TZ, T, n, bpos) : -1;
     nn_dist[rowoff + c] = bd;
   }
@@ -3644,7 +3651,7 @@ int rows_match_launch(navgpu_ctx *ctx, const double *src, const double *tgt, int
   }
   const RowsLds L = rows_lds(C, kRowsBlock, true);
   RC(set_lds(k_rows_match, L.total));
-  hipLaunchKernelGGL(k_rows_match, dim3(rows), dim3(kRowsBlock), L.total, ctx->stream, src,
+  hipLaunchKernelGGL(k_rows_match, dim3(rows), dim3(kRowsMatchBlock), L.total, ctx->stream, src,
                      tgt, R, C, src_mask, tgt_mask, nn_idx, nn_dist, tie, S);
   CHECK_LAUNCH("k_rows_match");
   return NAVGPU_OK;
