@@ -3632,22 +3632,31 @@ int rows_match_launch(navgpu_ctx *ctx, const double *src, const double *tgt, int
     tgt_mask = nullptr;
   }
   if (lean) {
-    const int walkers = rows_lean_walkers(tie != nullptr, 256);
+    // threads per row (NAVGPU_LEAN_NT = 256 | 512 | 1024; r6: K4 integer-mm
+    // 30.80 / 26.87 / 36.35 ms, profiles/r6/k4i_lean_threads_ab.txt)
+    static const int ntl = getenv("NAVGPU_LEAN_NT") ? atoi(getenv("NAVGPU_LEAN_NT")) : 512;
+    const int NTl = ntl == 1024 ? 1024 : (ntl == 256 ? 256 : 512);
+    const int walkers = rows_lean_walkers(tie != nullptr, NTl);
     const int F1 = std::min(C, kLeanF);
     int32_t *over;
     RC(ws(ctx, kOvf, rows, &over));
-    int lds = rows_lean_lds(C, F1, walkers);
-    RC(set_lds(k_rows_match_lean<256>, std::max(lds, rows_lean_lds(C, C, walkers))));
-    hipLaunchKernelGGL(k_rows_match_lean<256>, dim3(rows), dim3(256), lds, ctx->stream, src,
-                       tgt, R, C, src_mask, tgt_mask, nn_idx, nn_dist, tie, S, F1, over, 0);
-    CHECK_LAUNCH("k_rows_match_lean");
-    if (F1 < C) {  // the rows with more than F1 features
-      lds = rows_lean_lds(C, C, walkers);
-      hipLaunchKernelGGL(k_rows_match_lean<256>, dim3(rows), dim3(256), lds, ctx->stream, src,
-                         tgt, R, C, src_mask, tgt_mask, nn_idx, nn_dist, tie, S, C, over, 1);
+    auto launch = [&](auto kern, int F, int pass, int lds) -> int {
+      hipLaunchKernelGGL(kern, dim3(rows), dim3(NTl), lds, ctx->stream, src, tgt, R, C, src_mask,
+                         tgt_mask, nn_idx, nn_dist, tie, S, F, over, pass);
       CHECK_LAUNCH("k_rows_match_lean");
-    }
-    return NAVGPU_OK;
+      return NAVGPU_OK;
+    };
+    auto run = [&](auto kern) -> int {
+      int lds = rows_lean_lds(C, F1, walkers);
+      RC(set_lds(kern, std::max(lds, rows_lean_lds(C, C, walkers))));
+      RC(launch(kern, F1, 0, lds));
+      if (F1 < C)  // the rows with more than F1 features
+        RC(launch(kern, C, 1, rows_lean_lds(C, C, walkers)));
+      return NAVGPU_OK;
+    };
+    if (NTl == 1024) return run(k_rows_match_lean<1024>);
+    if (NTl == 512) return run(k_rows_match_lean<512>);
+    return run(k_rows_match_lean<256>);
   }
   const RowsLds L = rows_lds(C, kRowsBlock, true);
   RC(set_lds(k_rows_match, L.total));
